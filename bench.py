@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident CURVE MESSAGE encode+decode on MI355X.
+
+Metric (BASELINE.json): GiB/s device-resident CURVE encode+decode, 1 KiB-msg
+batches; msgs/s.  Workload at N=1 = BASELINE config 2: 65,536 x 1 KiB
+frames, one CURVE session, encode (zmqg_encode_batch) then decode
+(zmqg_decode_batch) of the produced wire frames, inputs resident in HBM.
+One step = one such round trip over the batch (fresh nonces every step:
+the decoder's replay rule would reject a repeated nonce).
+
+Multi-GPU (torchrun, one process per GPU): every rank runs the same
+per-GPU batch on its own device with its own sessions -- the path shards by
+frame with no data exchange (weak scaling).  Ranks meet only at the
+barriers around the timed region (gloo, control only).
+
+JSON line fields beyond the driver contract:
+  roofline      dominant kernel (decode body) achieved algorithmic HBM-read
+                GB/s vs the 8 TB/s peak, durations from HIP events recorded
+                live around that kernel on its stream during the timed steps;
+                traffic = PMC-measured HBM bytes per launch from
+                profiles/ if a PMC summary for this workload was committed.
+  cpu_baseline  the oracle's C restatement of curve_encoding_t with
+                libsodium's crypto_box_easy_afternm/open (dlopen) on host
+                threads, rank 0 at N=1 only, on a bounded sample.
+  host_staged   the same round trip through zmqg_*_host (pageable host
+                buffers, pinned staging, H2D + D2H): PCIe-inclusive rate.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--msgs", type=int, default=65536)
+    p.add_argument("--size", type=int, default=1024)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-staged", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of CPU baseline sampling")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from libzmq_amd import curve as C
+
+    n, P = args.msgs, args.size
+    W = C.wire_size(0, 0, P)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED + rank)
+    payload = torch.randint(0, 256, (n * P,), dtype=torch.uint8, device=dev, generator=g)
+    precom = torch.randint(0, 256, (32,), dtype=torch.uint8, generator=torch.Generator().manual_seed(0x5EED + rank))
+    precom = bytes(precom.tolist())
+
+    enc = C.CurveContext(local, 1)
+    enc.session_set(0, precom, C.CLIENT_PREFIX, C.SERVER_PREFIX)
+    dec = C.CurveContext(local, 1)
+    dec.session_set(0, precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+
+    i64 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    sid = i32(np.zeros(n, np.uint32))
+    flags_np = np.where(np.arange(n) % 16 == 15, 1, 0).astype(np.uint8)  # 1 in 16 with MORE
+    flags = torch.from_numpy(flags_np).to(dev)
+    in_off = i64(np.arange(n, dtype=np.uint64) * P)
+    lens = i32(np.full(n, P, np.uint32))
+    out_off = i64(np.arange(n, dtype=np.uint64) * W)
+    wlen = i32(np.full(n, W, np.uint32))
+    nonce = i64(np.arange(3, 3 + n, dtype=np.uint64))
+    wire = torch.zeros(n * W, dtype=torch.uint8, device=dev)
+    back = torch.zeros(n * P, dtype=torch.uint8, device=dev)
+    fl_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    st_out = torch.zeros(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        enc.encode_batch(sid, nonce, flags, in_off, lens, payload, out_off, wire, stream)
+        dec.decode_batch(sid, out_off, wlen, wire, in_off, back, fl_out, st_out, stream)
+        nonce.add_(n)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # correctness of the work being timed
+    assert int((st_out != 0).sum()) == 0, "decode failures in warmup"
+    assert torch.equal(back, payload), "round trip mismatch"
+    assert torch.equal(fl_out.cpu(), torch.from_numpy(flags_np)), "flags mismatch"
+
+    enc.set_profiling(True)
+    dec.set_profiling(True)
+    enc.get_profile(0), dec.get_profile(1)  # clear
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    enc_body_ms, enc_body_n = enc.get_profile(C.CurveContext.PROF_ENCODE_BODY)
+    dec_body_ms, dec_body_n = dec.get_profile(C.CurveContext.PROF_DECODE_BODY)
+    enc_call_ms, _ = enc.get_profile(C.CurveContext.PROF_ENCODE_CALL)
+    dec_call_ms, _ = dec.get_profile(C.CurveContext.PROF_DECODE_CALL)
+    enc.set_profiling(False)
+    dec.set_profiling(False)
+    assert int((st_out != 0).sum()) == 0
+    assert torch.equal(back, payload)
+
+    total_msgs = n * args.steps * world
+    gib = total_msgs * P / 2**30
+    value = gib / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # roofline of the dominant kernel: decode body.  Algorithmic HBM-read
+    # bytes of decode per frame: wire W + sid 4 + offset 8 +
+    # length 4 = P + 49.
+    dec_avg_s = dec_body_ms / max(dec_body_n, 1) / 1e3
+    enc_avg_s = enc_body_ms / max(enc_body_n, 1) / 1e3
+    dec_read = n * (P + 49)
+    achieved = dec_read / dec_avg_s / 1e9 if dec_avg_s > 0 else None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic_config2.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("k_decode_body_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "kernel": "k_decode_body", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None, "traffic": traffic,
+                "algorithmic_bytes_per_launch": dec_read, "avg_launch_us": dec_avg_s * 1e6,
+                "encode_body_avg_us": enc_avg_s * 1e6,
+                "encode_call_avg_us": enc_call_ms / max(enc_body_n, 1) * 1e3,
+                "decode_call_avg_us": dec_call_ms / max(dec_body_n, 1) * 1e3,
+                "path_read_frac": (n * (2 * P + 74)) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS * world
+                if world == 1 else None}
+
+    result = {
+        "metric": "GiB/s device-resident CURVE encode+decode, 1 KiB-msg batches; msgs/s",
+        "value": value,
+        "unit": "GiB/s",
+        "msgs_per_s": total_msgs / elapsed,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded random payload bytes, random precomputed key)",
+        "config": {"workload": f"config2: {n} x {P} B frames, 1 CURVE session per GPU, encode+decode round trip",
+                   "frames_per_gpu": n, "payload_bytes": P, "wire_bytes": W, "sessions": 1,
+                   "parallelism": f"frame-sharded x{world}, no collective"},
+        "roofline": roofline,
+    }
+
+    if rank == 0 and world == 1 and not args.no_host_staged:
+        # PCIe-inclusive: pageable host buffers through zmqg_*_host
+        hp = payload.cpu().numpy()
+        hin = np.arange(n, dtype=np.uint64) * P
+        hout = np.arange(n, dtype=np.uint64) * W
+        hctx = C.CurveContext(local, 1)
+        hctx.session_set(0, precom, C.CLIENT_PREFIX, C.SERVER_PREFIX)
+        hdec = C.CurveContext(local, 1)
+        hdec.session_set(0, precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+        z32 = np.zeros(n, np.uint32)
+        lens_h = np.full(n, P, np.uint32)
+        wl_h = np.full(n, W, np.uint32)
+        reps = 5
+        t0 = time.perf_counter()
+        for r in range(reps):
+            nn = np.arange(3 + r * n, 3 + (r + 1) * n, dtype=np.uint64)
+            w = hctx.encode_host(z32, nn, flags_np, hin, lens_h, hp, hout, n * W)
+            pl, _, st = hdec.decode_host(z32, hout, wl_h, w, hin, n * P)
+        t1 = time.perf_counter()
+        assert (st == 0).all() and np.array_equal(pl, hp)
+        result["host_staged"] = {"value": reps * n * P / 2**30 / (t1 - t0), "unit": "GiB/s",
+                                 "note": "zmqg_encode_host + zmqg_decode_host, pageable buffers, H2D+D2H included"}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(payload.cpu().numpy(), precom, n, P, W, flags_np, args.cpu_seconds)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(payload, precom, n, P, W, flags_np, seconds):
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    # sessions partitioned across threads (one I/O thread owns a connection)
+    S = threads
+    sess = O.make_sessions([precom] * S)
+    sid = (np.arange(n) % S).astype(np.uint32)
+    nonce = np.arange(3, 3 + n, dtype=np.uint64)
+    in_off = np.arange(n, dtype=np.uint64) * P
+    lens = np.full(n, P, np.uint32)
+    wire_off = np.arange(n, dtype=np.uint64) * W
+    kind = "libsodium 1.0.18 crypto_box_easy_afternm/open (dlopen)"
+    secs, ok = O.bench_roundtrip(True, threads, sess, sid, nonce, flags_np, in_off, lens, payload, wire_off, n * W)
+    use_sodium = secs is not None
+    if not use_sodium:
+        kind = "portable C XSalsa20-Poly1305 restatement"
+    total_s, passes, oks = 0.0, 0, 0
+    while total_s < seconds or passes < 2:
+        s, ok = O.bench_roundtrip(use_sodium, threads, sess, sid, nonce, flags_np, in_off, lens, payload, wire_off,
+                                  n * W)
+        total_s += s
+        passes += 1
+        oks += ok
+    assert oks == passes * n
+    return {"value": passes * n * P / 2**30 / total_s, "unit": "GiB/s", "cores": threads, "kind": "port",
+            "msgs_per_s": passes * n / total_s,
+            "sample": f"{passes} passes x {n} x {P} B encode+decode round trips ({total_s:.2f} s wall, "
+                      f"{threads} threads, {S} sessions); crypto: {kind}; framing: oracle/curve_oracle.c "
+                      f"restatement of curve_encoding_t"}
+
+
+if __name__ == "__main__":
+    main()

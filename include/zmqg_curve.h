@@ -1,0 +1,161 @@
+/*
+ * zmqg_curve.h -- C ABI of the MI355X CurveZMQ MESSAGE AEAD path.
+ *
+ * This is the drop-in boundary for libzmq's CURVE message codec:
+ *
+ *   reference call                                   replaced by
+ *   -----------------------------------------------  ---------------------------
+ *   curve_encoding_t::encode
+ *     src/curve_mechanism_base.cpp:111-205           zmqg_encode_batch
+ *     (crypto_box_easy_afternm :172-174)
+ *   curve_mechanism_base_t::decode
+ *     src/curve_mechanism_base.cpp:38-52             zmqg_decode_batch
+ *     check_basic_command_structure
+ *       src/mechanism_base.cpp:14-25
+ *     curve_encoding_t::decode / check_validity
+ *       src/curve_mechanism_base.cpp:80-109, 207-284
+ *     (crypto_box_open_easy_afternm :226-228)
+ *   curve_encoding_t state (_cn_precom, prefixes,
+ *     _downgrade_sub, _cn_peer_nonce)
+ *     src/curve_mechanism_base.hpp:44-58             zmqg_session_set,
+ *                                                    zmqg_session_*_peer_nonce
+ *   curve_encoding_t::get_writable_precom_buffer
+ *     src/curve_mechanism_base.hpp:36                zmqg_session_set (precom)
+ *   curve_encoding_t::set_peer_nonce
+ *     src/curve_mechanism_base.hpp:42                zmqg_session_set_peer_nonce
+ *
+ * One call processes a batch of independent MESSAGE frames.  Each frame
+ * belongs to a session (one CURVE connection = one curve_encoding_t).  The
+ * caller assigns encode nonces (the reference's get_and_inc_nonce,
+ * src/curve_mechanism_base.hpp:41).  Decode applies the reference's replay
+ * rule exactly as if curve_encoding_t::decode had been called on the batch's
+ * frames one by one in batch order, and updates each session's peer nonce.
+ *
+ * Conventions
+ *   - Return 0 on success, a negative errno value on failure (-EINVAL bad
+ *     argument, -ENOMEM, -EIO a HIP runtime error).  Per-frame protocol
+ *     errors are not call failures: they are reported in status_out with the
+ *     reference's codes (ZMQ_PROTOCOL_ERROR_ZMTP_*, include/zmq.h:424-437).
+ *   - Batch pointers (descriptors, in, out, flags_out, status_out) must be
+ *     device memory of the ctx's device, or host memory the device can
+ *     access (hipHostMalloc).  Batch calls are asynchronous on `stream`
+ *     (a hipStream_t; NULL = the null stream); results are valid once the
+ *     stream has been synchronised.
+ *   - A ctx is externally synchronised, like the reference's mechanism (one
+ *     I/O thread per connection): issue one ctx's batches on one stream.
+ *   - No exceptions cross this boundary.
+ */
+#ifndef ZMQG_CURVE_H_INCLUDED
+#define ZMQG_CURVE_H_INCLUDED
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZMQG_CURVE_ABI_VERSION 1
+
+/* Per-frame status codes, identical to include/zmq.h:424-437. */
+#define ZMQG_STATUS_OK 0
+#define ZMQG_ERR_UNEXPECTED_COMMAND 0x10000001  /* ZMQ_PROTOCOL_ERROR_ZMTP_UNEXPECTED_COMMAND */
+#define ZMQG_ERR_INVALID_SEQUENCE 0x10000002    /* ZMQ_PROTOCOL_ERROR_ZMTP_INVALID_SEQUENCE */
+#define ZMQG_ERR_MALFORMED_UNSPECIFIED 0x10000011 /* ..._MALFORMED_COMMAND_UNSPECIFIED */
+#define ZMQG_ERR_MALFORMED_MESSAGE 0x10000012   /* ..._MALFORMED_COMMAND_MESSAGE */
+#define ZMQG_ERR_CRYPTOGRAPHIC 0x11000001       /* ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC */
+
+/* msg_t flag bits used on this path (src/msg.hpp:55-62). */
+#define ZMQG_MSG_MORE 1
+#define ZMQG_MSG_COMMAND 2
+#define ZMQG_MSG_SUBSCRIBE 12
+#define ZMQG_MSG_CANCEL 16
+
+typedef struct zmqg_ctx zmqg_ctx;
+
+/* ABI version of the loaded library (== ZMQG_CURVE_ABI_VERSION). */
+int zmqg_abi_version(void);
+
+/* Create a context on HIP device `device` with a session table of
+ * `max_sessions` entries (sids 0 .. max_sessions-1). */
+int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out);
+int zmqg_ctx_destroy(zmqg_ctx *ctx);
+
+/* Install session `sid`: the connection's precomputed key (_cn_precom, the
+ * output of crypto_box_beforenm, src/curve_client_tools.hpp:105 /
+ * src/curve_server.cpp:382-383), the 16-byte encode/decode nonce prefixes
+ * ("CurveZMQMESSAGEC"/"CurveZMQMESSAGES" swapped per side,
+ * src/curve_client.cpp:22-23, src/curve_server.cpp:24-25), the downgrade_sub
+ * flag (src/zmtp_engine.cpp:339-351) and the initial peer nonce (the
+ * reference starts at 1 and the handshake advances it).  The two XSalsa20
+ * subkeys HSalsa20(precom, prefix) are derived on the device.  Synchronous. */
+int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], const uint8_t enc_prefix[16],
+                     const uint8_t dec_prefix[16], int downgrade_sub, uint64_t peer_nonce);
+
+/* curve_encoding_t::set_peer_nonce / read back _cn_peer_nonce.  Synchronous
+ * (they order after all work previously issued on the ctx's last stream). */
+int zmqg_session_set_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t peer_nonce);
+int zmqg_session_get_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *peer_nonce_out);
+
+/* Bytes of the encoded frame for a payload of `payload_len` bytes and msg_t
+ * flags `msg_flags`: "\x07MESSAGE"(8) + nonce(8) + tag(16) + mlen, where
+ * mlen = 1 + [1 | 7 | 10 for SUBSCRIBE/CANCEL] + payload_len
+ * (src/curve_mechanism_base.cpp:113-128, 169). */
+uint64_t zmqg_wire_size(uint8_t msg_flags, int downgrade_sub, uint64_t payload_len);
+
+/* Encode n frames (curve_encoding_t::encode).  Frame i: session sid[i],
+ * nonce nonce[i], msg_t flags flags[i], payload in[in_off[i] .. +len[i]).
+ * Writes zmqg_wire_size(flags[i], session.downgrade_sub, len[i]) bytes at
+ * out[out_off[i]]: "\x07MESSAGE" || BE64(nonce) || tag || ciphertext.
+ * Output frames must not overlap each other or the input. */
+int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                      const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                      uint8_t *out, void *stream);
+
+/* Decode n frames (curve_mechanism_base_t::decode).  Frame i: session sid[i],
+ * wire bytes in[in_off[i] .. +wire_len[i]).  On success status_out[i] = 0,
+ * flags_out[i] = plaintext flags & (MORE|COMMAND) (the caller ORs them into
+ * the msg_t, as msg_t::set_flags does, src/msg.cpp:433-436) and the payload,
+ * wire_len[i] - 33 bytes, is written at out[out_off[i]].  On failure
+ * status_out[i] is the reference's error code, flags_out[i] = 0 and, when
+ * wire_len[i] >= 33, the payload region is zero-filled: plaintext of a frame
+ * that failed is never left in `out`.  Each session's peer nonce advances as
+ * the reference's check_validity does (src/curve_mechanism_base.cpp:98-106,
+ * including on a later MAC failure).  `out` must not overlap `in`. */
+int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                      const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
+                      uint8_t *flags_out, int32_t *status_out, void *stream);
+
+/* Host-memory convenience forms of the two batch calls: every pointer is
+ * ordinary (pageable) host memory.  They stage through the ctx's pinned
+ * buffers with hipMemcpyAsync H2D, run the batch and copy back D2H, and
+ * return after the stream has synchronised.  This is the path an I/O thread
+ * calling with socket buffers takes. */
+int zmqg_encode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                     const uint64_t *in_off, const uint32_t *len, const uint8_t *in, uint64_t in_bytes,
+                     const uint64_t *out_off, uint8_t *out, uint64_t out_bytes);
+int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                     const uint32_t *wire_len, const uint8_t *in, uint64_t in_bytes, const uint64_t *out_off,
+                     uint8_t *out, uint64_t out_bytes, uint8_t *flags_out, int32_t *status_out);
+
+/* Profiling hooks (off by default).  When enabled, the ctx records a HIP
+ * event pair on the batch's stream around each of its kernels of one kind:
+ *   ZMQG_PROF_ENCODE_BODY / ZMQG_PROF_DECODE_BODY  the body kernel alone,
+ *   ZMQG_PROF_ENCODE_CALL / ZMQG_PROF_DECODE_CALL  the whole batch call.
+ * zmqg_ctx_get_profile synchronises the device, returns the summed elapsed
+ * milliseconds and launch count for `kind` since the last reset, and resets. */
+#define ZMQG_PROF_ENCODE_BODY 0
+#define ZMQG_PROF_DECODE_BODY 1
+#define ZMQG_PROF_ENCODE_CALL 2
+#define ZMQG_PROF_DECODE_CALL 3
+int zmqg_ctx_set_profiling(zmqg_ctx *ctx, int enable);
+int zmqg_ctx_get_profile(zmqg_ctx *ctx, int kind, double *ms_total, uint64_t *launches);
+
+/* Text for the last HIP error seen by this ctx (static storage). */
+const char *zmqg_last_error(zmqg_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

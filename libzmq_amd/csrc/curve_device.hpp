@@ -1,0 +1,387 @@
+// curve_device.hpp -- device-side building blocks of the CURVE MESSAGE path
+// for gfx950: Salsa20/HSalsa20 keystream, radix-2^26 Poly1305 field
+// arithmetic, and byte-exact loads/stores of arbitrarily aligned 64-byte
+// windows.
+//
+// Algorithms: XSalsa20 and Poly1305 as composed by NaCl/libsodium 1.0.18
+// crypto_box_easy_afternm (the call at reference
+// src/curve_mechanism_base.cpp:172-174): keystream block 0 bytes 0..31 are
+// the Poly1305 key, plaintext byte i is XORed with keystream byte 32+i.
+// Everything here is 32-bit integer VALU work: v_add/v_xor/v_alignbit for
+// Salsa20, v_mad_u64_u32 for the Poly1305 limb products.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zmqg {
+
+// ---------------------------------------------------------------- Salsa20
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t n)
+{
+    return __builtin_rotateleft32(x, n); // one v_alignbit_b32
+}
+
+#define ZMQG_QR(a, b, c, d)        \
+    b ^= rotl32(a + d, 7);         \
+    c ^= rotl32(b + a, 9);         \
+    d ^= rotl32(c + b, 13);        \
+    a ^= rotl32(d + c, 18);
+
+// 20 rounds (10 column + row double rounds) over 16 registers.
+#define ZMQG_SALSA20_ROUNDS(x)                                   \
+    _Pragma("unroll") for (int rr_ = 0; rr_ < 10; ++rr_)         \
+    {                                                            \
+        ZMQG_QR(x[0], x[4], x[8], x[12]);                        \
+        ZMQG_QR(x[5], x[9], x[13], x[1]);                        \
+        ZMQG_QR(x[10], x[14], x[2], x[6]);                       \
+        ZMQG_QR(x[15], x[3], x[7], x[11]);                       \
+        ZMQG_QR(x[0], x[1], x[2], x[3]);                         \
+        ZMQG_QR(x[5], x[6], x[7], x[4]);                         \
+        ZMQG_QR(x[10], x[11], x[8], x[9]);                       \
+        ZMQG_QR(x[15], x[12], x[13], x[14]);                     \
+    }
+
+constexpr uint32_t SIGMA0 = 0x61707865, SIGMA1 = 0x3320646e, SIGMA2 = 0x79622d32, SIGMA3 = 0x6b206574;
+
+// Keystream block `ctr` of Salsa20/20 under subkey k[8] and 8-byte nonce
+// (n0, n1 = the nonce bytes as little-endian words).
+__device__ __forceinline__ void salsa20_block(uint32_t out[16], const uint32_t k[8], uint32_t n0, uint32_t n1,
+                                              uint32_t ctr_lo, uint32_t ctr_hi)
+{
+    uint32_t x[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1,
+                      ctr_lo, ctr_hi, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+    ZMQG_SALSA20_ROUNDS(x);
+    out[0] = x[0] + SIGMA0;
+    out[1] = x[1] + k[0];
+    out[2] = x[2] + k[1];
+    out[3] = x[3] + k[2];
+    out[4] = x[4] + k[3];
+    out[5] = x[5] + SIGMA1;
+    out[6] = x[6] + n0;
+    out[7] = x[7] + n1;
+    out[8] = x[8] + ctr_lo;
+    out[9] = x[9] + ctr_hi;
+    out[10] = x[10] + SIGMA2;
+    out[11] = x[11] + k[4];
+    out[12] = x[12] + k[5];
+    out[13] = x[13] + k[6];
+    out[14] = x[14] + k[7];
+    out[15] = x[15] + SIGMA3;
+}
+
+// HSalsa20(k, in[4 words]) -> 8-word subkey (no feed-forward).
+__device__ __forceinline__ void hsalsa20(uint32_t out[8], const uint32_t k[8], const uint32_t in[4])
+{
+    uint32_t x[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, in[0], in[1],
+                      in[2], in[3], SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+    ZMQG_SALSA20_ROUNDS(x);
+    out[0] = x[0];
+    out[1] = x[5];
+    out[2] = x[10];
+    out[3] = x[15];
+    out[4] = x[6];
+    out[5] = x[7];
+    out[6] = x[8];
+    out[7] = x[9];
+}
+
+// ---------------------------------------------------------------- Poly1305
+// Field elements mod 2^130-5 in five 26-bit limbs.  "Partially reduced":
+// every limb < 2^26 except limb 1, which may exceed it by a few bits.
+constexpr uint32_t M26 = 0x3ffffff;
+
+struct fe {
+    uint32_t l[5];
+};
+
+__device__ __forceinline__ fe fe_zero()
+{
+    fe z;
+    z.l[0] = z.l[1] = z.l[2] = z.l[3] = z.l[4] = 0;
+    return z;
+}
+
+__device__ __forceinline__ fe fe_one()
+{
+    fe o = fe_zero();
+    o.l[0] = 1;
+    return o;
+}
+
+// r from the first 16 keystream bytes, clamped
+// (r &= 0x0ffffffc0ffffffc0ffffffc0fffffff), split into 26-bit limbs.
+__device__ __forceinline__ fe poly_r_from_key(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3)
+{
+    fe r;
+    r.l[0] = k0 & 0x3ffffff;
+    r.l[1] = __builtin_amdgcn_alignbit(k1, k0, 26) & 0x3ffff03;
+    r.l[2] = __builtin_amdgcn_alignbit(k2, k1, 20) & 0x3ffc0ff;
+    r.l[3] = __builtin_amdgcn_alignbit(k3, k2, 14) & 0x3f03fff;
+    r.l[4] = (k3 >> 8) & 0x00fffff;
+    return r;
+}
+
+// h += 16-byte block (m0..m3 little-endian words) + hibit*2^128.
+__device__ __forceinline__ void fe_add_block(fe &h, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                             uint32_t hibit)
+{
+    h.l[0] += m0 & M26;
+    h.l[1] += __builtin_amdgcn_alignbit(m1, m0, 26) & M26;
+    h.l[2] += __builtin_amdgcn_alignbit(m2, m1, 20) & M26;
+    h.l[3] += __builtin_amdgcn_alignbit(m3, m2, 14) & M26;
+    h.l[4] += (m3 >> 8) | hibit;
+}
+
+__device__ __forceinline__ void fe_add(fe &h, const fe &x)
+{
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        h.l[i] += x.l[i];
+}
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c)
+{
+    return (uint64_t) a * b + c; // v_mad_u64_u32
+}
+
+// h = h * r mod 2^130-5, partially reduced.  s = 5*r[1..4] precomputed.
+// Inputs: h limbs < 2^27, r limbs < 2^26 + 2^8.
+__device__ __forceinline__ void fe_mul_s(fe &h, const fe &r, const uint32_t s1, const uint32_t s2, const uint32_t s3,
+                                         const uint32_t s4)
+{
+    const uint32_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4];
+    uint64_t d0 = mad64(h4, s1, mad64(h3, s2, mad64(h2, s3, mad64(h1, s4, (uint64_t) h0 * r.l[0]))));
+    uint64_t d1 = mad64(h4, s2, mad64(h3, s3, mad64(h2, s4, mad64(h1, r.l[0], (uint64_t) h0 * r.l[1]))));
+    uint64_t d2 = mad64(h4, s3, mad64(h3, s4, mad64(h2, r.l[0], mad64(h1, r.l[1], (uint64_t) h0 * r.l[2]))));
+    uint64_t d3 = mad64(h4, s4, mad64(h3, r.l[0], mad64(h2, r.l[1], mad64(h1, r.l[2], (uint64_t) h0 * r.l[3]))));
+    uint64_t d4 = mad64(h4, r.l[0], mad64(h3, r.l[1], mad64(h2, r.l[2], mad64(h1, r.l[3], (uint64_t) h0 * r.l[4]))));
+    uint32_t c;
+    c = (uint32_t) (d0 >> 26);
+    h.l[0] = (uint32_t) d0 & M26;
+    d1 += c;
+    c = (uint32_t) (d1 >> 26);
+    h.l[1] = (uint32_t) d1 & M26;
+    d2 += c;
+    c = (uint32_t) (d2 >> 26);
+    h.l[2] = (uint32_t) d2 & M26;
+    d3 += c;
+    c = (uint32_t) (d3 >> 26);
+    h.l[3] = (uint32_t) d3 & M26;
+    d4 += c;
+    c = (uint32_t) (d4 >> 26);
+    h.l[4] = (uint32_t) d4 & M26;
+    h.l[0] += c * 5;
+    c = h.l[0] >> 26;
+    h.l[0] &= M26;
+    h.l[1] += c;
+}
+
+__device__ __forceinline__ void fe_mul(fe &h, const fe &r)
+{
+    fe_mul_s(h, r, r.l[1] * 5, r.l[2] * 5, r.l[3] * 5, r.l[4] * 5);
+}
+
+// Fold 64-bit limb sums (from lane reductions / atomics) back to a
+// partially reduced element.
+__device__ __forceinline__ fe fe_from_wide(const uint64_t w[5])
+{
+    uint64_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = w[4];
+    a1 += a0 >> 26;
+    a0 &= M26;
+    a2 += a1 >> 26;
+    a1 &= M26;
+    a3 += a2 >> 26;
+    a2 &= M26;
+    a4 += a3 >> 26;
+    a3 &= M26;
+    a0 += (a4 >> 26) * 5;
+    a4 &= M26;
+    a1 += a0 >> 26;
+    a0 &= M26;
+    fe h;
+    h.l[0] = (uint32_t) a0;
+    h.l[1] = (uint32_t) a1;
+    h.l[2] = (uint32_t) a2;
+    h.l[3] = (uint32_t) a3;
+    h.l[4] = (uint32_t) a4;
+    return h;
+}
+
+// Freeze h mod 2^130-5 and add the pad s (mod 2^128): the tag, as 4 words.
+__device__ __forceinline__ void poly_finish(fe h, const uint32_t s[4], uint32_t tag[4])
+{
+    uint32_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4], c;
+    c = h1 >> 26;
+    h1 &= M26;
+    h2 += c;
+    c = h2 >> 26;
+    h2 &= M26;
+    h3 += c;
+    c = h3 >> 26;
+    h3 &= M26;
+    h4 += c;
+    c = h4 >> 26;
+    h4 &= M26;
+    h0 += c * 5;
+    c = h0 >> 26;
+    h0 &= M26;
+    h1 += c;
+    uint32_t g0 = h0 + 5;
+    c = g0 >> 26;
+    g0 &= M26;
+    uint32_t g1 = h1 + c;
+    c = g1 >> 26;
+    g1 &= M26;
+    uint32_t g2 = h2 + c;
+    c = g2 >> 26;
+    g2 &= M26;
+    uint32_t g3 = h3 + c;
+    c = g3 >> 26;
+    g3 &= M26;
+    uint32_t g4 = h4 + c - (1u << 26);
+    const uint32_t mask = (g4 >> 31) - 1u;
+    h0 = (h0 & ~mask) | (g0 & mask);
+    h1 = (h1 & ~mask) | (g1 & mask);
+    h2 = (h2 & ~mask) | (g2 & mask);
+    h3 = (h3 & ~mask) | (g3 & mask);
+    h4 = (h4 & ~mask) | (g4 & mask);
+    uint64_t f0 = (uint64_t) (h0 | (h1 << 26)) + s[0];
+    uint64_t f1 = (uint64_t) ((h1 >> 6) | (h2 << 20)) + s[1] + (f0 >> 32);
+    uint64_t f2 = (uint64_t) ((h2 >> 12) | (h3 << 14)) + s[2] + (f1 >> 32);
+    uint64_t f3 = (uint64_t) ((h3 >> 18) | (h4 << 8)) + s[3] + (f2 >> 32);
+    tag[0] = (uint32_t) f0;
+    tag[1] = (uint32_t) f1;
+    tag[2] = (uint32_t) f2;
+    tag[3] = (uint32_t) f3;
+}
+
+// Poly1305-absorb 16 words (64 bytes) of which `nv` bytes are valid,
+// as up to four 16-byte blocks; a partial final block is padded 0x01 0...
+// Bytes beyond nv in w[] must already be zero.
+__device__ __forceinline__ void poly_absorb64(fe &h, const fe &r, const uint32_t s1, const uint32_t s2,
+                                              const uint32_t s3, const uint32_t s4, uint32_t w[16], int nv)
+{
+    if (nv >= 64) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            fe_add_block(h, w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], 1u << 24);
+            fe_mul_s(h, r, s1, s2, s3, s4);
+        }
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int bl = nv - 16 * q;
+        if (bl <= 0)
+            break;
+        uint32_t m[4] = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+        uint32_t hibit = 1u << 24;
+        if (bl < 16) {
+            hibit = 0;
+            const int wi = bl >> 2, bi = bl & 3;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (t == wi)
+                    m[t] |= 1u << (8 * bi);
+        }
+        fe_add_block(h, m[0], m[1], m[2], m[3], hibit);
+        fe_mul_s(h, r, s1, s2, s3, s4);
+    }
+}
+
+// ---------------------------------------------------------------- bytes
+// Little-endian word of 4 bytes from a byte pointer (any alignment).
+__device__ __forceinline__ uint32_t bswap32(uint32_t x)
+{
+    return __builtin_bswap32(x);
+}
+
+// Zero bytes >= nv of a 16-word window.
+__device__ __forceinline__ void mask_tail(uint32_t w[16], int nv)
+{
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int b = nv - 4 * i;
+        const uint32_t m = b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+        w[i] &= m;
+    }
+}
+
+// Load bytes p[0 .. nv) (0 <= nv <= 64, any alignment) as 16 little-endian
+// words, zero beyond nv.  Only 4-byte words that hold a valid byte are read,
+// so the access never leaves the 4-byte granules of the valid range.
+__device__ __forceinline__ void load_window(const uint8_t *p, int nv, uint32_t w[16])
+{
+    const uintptr_t a = (uintptr_t) p;
+    const uint32_t *q = (const uint32_t *) (a & ~(uintptr_t) 3);
+    const uint32_t sh = (uint32_t) (a & 3);
+    uint32_t d[17];
+    if (nv >= 64) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            d[i] = q[i];
+        d[16] = sh ? q[16] : 0u;
+    } else {
+        const int nd = (int) ((sh + (uint32_t) nv + 3) >> 2);
+#pragma unroll
+        for (int i = 0; i < 17; ++i)
+            d[i] = i < nd ? q[i] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    if (nv < 64)
+        mask_tail(w, nv);
+}
+
+// Store bytes w[0 .. nv) (as a little-endian byte stream) at p (any
+// alignment).  Only bytes [p, p+nv) are written: up to 3 leading and 3
+// trailing bytes by byte stores, the rest as aligned dword stores.
+__device__ __forceinline__ void store_window(uint8_t *p, int nv, const uint32_t w[16])
+{
+    const uintptr_t a = (uintptr_t) p;
+    const uint32_t sh = (uint32_t) (a & 3);
+    if (sh == 0 && nv >= 64) {
+        uint32_t *q = (uint32_t *) p;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            q[i] = w[i];
+        return;
+    }
+    const uint32_t s = (4u - sh) & 3u; // bytes before the first aligned dword
+    uint32_t e[16];
+#pragma unroll
+    for (int k = 0; k < 15; ++k)
+        e[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], s);
+    e[15] = __builtin_amdgcn_alignbyte(0u, w[15], s);
+    const int lead = (int) s < nv ? (int) s : nv;
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+        if (b < lead)
+            p[b] = (uint8_t) (w[0] >> (8 * b));
+    if (nv <= (int) s)
+        return;
+    const int rem = nv - (int) s;
+    const int nd = rem >> 2;
+    uint32_t *q = (uint32_t *) (a + s);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < nd)
+            q[k] = e[k];
+    const int tb = rem & 3;
+    if (tb) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (k == nd)
+                t = e[k];
+        uint8_t *pt = (uint8_t *) (q + nd);
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+            if (b < tb)
+                pt[b] = (uint8_t) (t >> (8 * b));
+    }
+}
+
+} // namespace zmqg

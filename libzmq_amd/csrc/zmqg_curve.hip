@@ -1,0 +1,1232 @@
+// zmqg_curve.hip -- batched CurveZMQ MESSAGE encode/decode for MI355X (gfx950).
+//
+// Replaces, for a batch of frames at once, reference
+// src/curve_mechanism_base.cpp:80-284 (curve_encoding_t::encode / decode /
+// check_validity, which call libsodium crypto_box_easy_afternm and
+// crypto_box_open_easy_afternm) and src/mechanism_base.cpp:14-25.
+// The C ABI is include/zmqg_curve.h.
+//
+// Work decomposition:
+//   head kernel   one lane per frame: header checks, keystream block 0
+//                 (Poly1305 key r,s + first 32 ciphertext bytes), the powers
+//                 of r the body needs, and the frame's body chunk count.
+//   chunk scan    inclusive prefix sum of chunk counts (hipCUB).
+//   replay scan   decode only: per-session exclusive prefix max of accepted
+//                 nonces in batch order (hipCUB), = the reference's
+//                 sequential _cn_peer_nonce rule.
+//   body kernel   one lane per chunk = 4 Salsa20 blocks = 256 ciphertext
+//                 bytes = 16 Poly1305 blocks; lanes of a frame are adjacent,
+//                 so the per-chunk Poly1305 partials (each multiplied by its
+//                 power of r) are summed by a segmented wave reduction and
+//                 the segment leader finishes the tag; frames spanning
+//                 several waves combine through 64-bit atomics and an
+//                 arrival counter (last arriver finishes).
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/zmqg_curve.h"
+#include "curve_device.hpp"
+
+using namespace zmqg;
+
+namespace {
+
+constexpr int kMaxPow = 24;           // r^(16*2^k), k < 24: frames up to 2^32 bytes
+constexpr uint32_t kIdle = 0xffffffffu;
+constexpr int kBodyThreads = 256;
+constexpr int kHeadThreads = 256;
+
+struct DevSession {
+    uint32_t enc_key[8]; // HSalsa20(precom, enc_prefix)
+    uint32_t dec_key[8]; // HSalsa20(precom, dec_prefix)
+    uint32_t downgrade_sub;
+    uint32_t pad[7];
+};
+
+// Per-frame state written by the head kernel, read by the body kernel.
+struct __attribute__((aligned(16))) MsgState {
+    uint32_t r[5];  // Poly1305 r (clamped), 26-bit limbs
+    uint32_t nch;   // body chunks (>= 1; a frame with no body bytes gets one empty chunk)
+    uint32_t s[4];  // Poly1305 pad
+    uint32_t hh[5]; // head blocks' Horner value times r^(body blocks)
+    uint32_t mlen;  // boxed plaintext length (flags + sub/cancel + payload)
+    uint32_t rb[5]; // r^(Poly1305 blocks in the last chunk)
+    uint32_t hl;    // encode: plaintext header length (1, 2, 8 or 11)
+    int32_t status; // decode: header status (0 = header ok)
+    uint32_t flags; // decode: plaintext flags & 3
+    uint32_t tag[4];   // decode: tag carried on the wire
+    uint64_t nonce;    // decode: wire nonce
+    uint64_t peer_snap; // decode: session peer nonce before this batch
+};
+static_assert(sizeof(MsgState) == 128, "MsgState layout");
+
+struct Workspace {
+    uint64_t cap = 0; // frames
+    MsgState *state = nullptr;
+    uint32_t *powtab = nullptr;   // [cap][kMaxPow][5]
+    unsigned long long *acc = nullptr; // [cap][5]
+    uint32_t *cnt = nullptr;      // [cap]
+    uint32_t *nch = nullptr;      // [cap]
+    uint32_t *chunk_end = nullptr; // [cap]
+    unsigned long long *v = nullptr;     // [cap] accepted nonce or 0
+    unsigned long long *excl = nullptr;  // [cap]
+    unsigned long long *v_s = nullptr;   // [cap] sorted
+    unsigned long long *excl_s = nullptr; // [cap]
+    uint32_t *iota = nullptr;     // [cap]
+    uint32_t *perm = nullptr;     // [cap]
+    uint32_t *keys_s = nullptr;   // [cap]
+    uint8_t *last = nullptr;      // [cap] last frame of its session in the batch
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+};
+
+} // namespace
+
+struct zmqg_ctx {
+    int device = 0;
+    uint32_t max_sessions = 0;
+    int sort_bits = 0;
+    DevSession *sessions = nullptr;
+    unsigned long long *peer = nullptr; // [max_sessions]
+    Workspace ws;
+    // host staging for the *_host entry points
+    uint8_t *pin = nullptr;
+    size_t pin_bytes = 0;
+    uint8_t *dbuf = nullptr;
+    size_t dbuf_bytes = 0;
+    hipStream_t own_stream = nullptr;
+    std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
+    // profiling: event pairs per kind, recycled through a pool
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[4];
+    std::vector<hipEvent_t> event_pool;
+    char last_error[256] = {0};
+    std::mutex mu;
+};
+
+#define ZCHECK(ctx, expr)                                                                      \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            snprintf((ctx)->last_error, sizeof((ctx)->last_error), "%s:%d %s: %s", __FILE__,   \
+                     __LINE__, #expr, hipGetErrorString(e_));                                  \
+            return -EIO;                                                               \
+        }                                                                                      \
+    } while (0)
+
+// =====================================================================
+// device helpers
+// =====================================================================
+namespace {
+
+__device__ __forceinline__ fe load_fe(const uint32_t *p)
+{
+    fe x;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        x.l[i] = p[i];
+    return x;
+}
+
+__device__ __forceinline__ void store_fe(uint32_t *p, const fe &x)
+{
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        p[i] = x.l[i];
+}
+
+// Number of Poly1305 blocks in the last body chunk, and body chunk count.
+__device__ __forceinline__ void body_geometry(uint32_t mlen, uint32_t &nch, uint32_t &blast)
+{
+    if (mlen <= 32) {
+        nch = 1;
+        blast = 0;
+        return;
+    }
+    const uint32_t body = mlen - 32;
+    nch = (body + 255) / 256;
+    const uint32_t lastb = body - 256 * (nch - 1);
+    blast = (lastb + 15) / 16;
+}
+
+// Computes and stores r^(16*2^k) for k < bits(nch-1), r^blast, and returns
+// the head factor r^(body blocks) = r^blast * (r^16)^(nch-1).
+__device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, uint32_t *powtab, fe &rb, fe &head_factor)
+{
+    fe r2 = r;
+    fe_mul(r2, r);
+    fe r4 = r2;
+    fe_mul(r4, r2);
+    fe r8 = r4;
+    fe_mul(r8, r4);
+    fe r16 = r8;
+    fe_mul(r16, r8);
+    rb = fe_one();
+    if (blast == 16) {
+        rb = r16;
+    } else {
+        if (blast & 1)
+            fe_mul(rb, r);
+        if (blast & 2)
+            fe_mul(rb, r2);
+        if (blast & 4)
+            fe_mul(rb, r4);
+        if (blast & 8)
+            fe_mul(rb, r8);
+    }
+    head_factor = rb;
+    uint32_t m = nch - 1; // head multiplies by (r^16)^(nch-1)
+    fe t = r16;
+    int k = 0;
+    while ((m >> k) != 0) {
+        store_fe(powtab + 5 * k, t);
+        if ((m >> k) & 1)
+            fe_mul(head_factor, t);
+        fe t2 = t;
+        fe_mul(t2, t);
+        t = t2;
+        ++k;
+    }
+    // body chunk 0 needs bits of nch-2 < nch-1: already covered.
+}
+
+// plaintext header of src/curve_mechanism_base.cpp:118-158 as 3 words
+__device__ __forceinline__ uint32_t plaintext_header(uint32_t msg_flags, uint32_t downgrade, uint32_t hw[3])
+{
+    const uint32_t f = msg_flags & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND);
+    const uint32_t ct = msg_flags & 0x1c;
+    const bool sub = ct == ZMQG_MSG_SUBSCRIBE, cancel = ct == ZMQG_MSG_CANCEL;
+    hw[1] = hw[2] = 0;
+    if (!(sub || cancel)) {
+        hw[0] = f;
+        return 1;
+    }
+    if (downgrade) {
+        hw[0] = f | ((sub ? 1u : 0u) << 8);
+        return 2;
+    }
+    if (cancel) { // f|2, "\x06CANCEL"
+        hw[0] = (f | 2u) | (6u << 8) | ((uint32_t) 'C' << 16) | ((uint32_t) 'A' << 24);
+        hw[1] = (uint32_t) 'N' | ((uint32_t) 'C' << 8) | ((uint32_t) 'E' << 16) | ((uint32_t) 'L' << 24);
+        return 8;
+    }
+    // f|2, "\x09SUBSCRIBE"
+    hw[0] = (f | 2u) | (9u << 8) | ((uint32_t) 'S' << 16) | ((uint32_t) 'U' << 24);
+    hw[1] = (uint32_t) 'B' | ((uint32_t) 'S' << 8) | ((uint32_t) 'C' << 16) | ((uint32_t) 'R' << 24);
+    hw[2] = (uint32_t) 'I' | ((uint32_t) 'B' << 8) | ((uint32_t) 'E' << 16);
+    return 11;
+}
+
+// out[i] = stream bytes of p shifted right by HL bytes (zeros shifted in), 8 words.
+template <int HL>
+__device__ __forceinline__ void shift_in(const uint32_t p[16], uint32_t out[8])
+{
+    constexpr int A = HL >> 2, B = HL & 3;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t hi = (i - A >= 0) ? p[i - A] : 0u;
+        const uint32_t lo = (i - A - 1 >= 0) ? p[i - A - 1] : 0u;
+        out[i] = B == 0 ? hi : __builtin_amdgcn_alignbyte(hi, lo, 4 - B);
+    }
+}
+
+__device__ __forceinline__ uint32_t lower_bound_chunk(const uint32_t *chunk_end, uint32_t n, uint32_t g)
+{
+    // first i with chunk_end[i] > g
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (chunk_end[mid] > g)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo;
+}
+
+// =====================================================================
+// session setup
+// =====================================================================
+__global__ void k_session_setup(DevSession *tab, unsigned long long *peer, uint32_t sid, const uint32_t *in)
+{
+    // in: precom[8] enc_prefix[4] dec_prefix[4] downgrade peer_lo peer_hi
+    if (threadIdx.x != 0)
+        return;
+    uint32_t k[8];
+    for (int i = 0; i < 8; ++i)
+        k[i] = in[i];
+    DevSession s;
+    hsalsa20(s.enc_key, k, in + 8);
+    hsalsa20(s.dec_key, k, in + 12);
+    s.downgrade_sub = in[16];
+    for (int i = 0; i < 7; ++i)
+        s.pad[i] = 0;
+    tab[sid] = s;
+    peer[sid] = ((unsigned long long) in[18] << 32) | in[17];
+}
+
+__global__ void k_set_peer(unsigned long long *peer, uint32_t sid, unsigned long long v)
+{
+    if (threadIdx.x == 0)
+        peer[sid] = v;
+}
+
+// =====================================================================
+// encode
+// =====================================================================
+__global__ __launch_bounds__(kHeadThreads) void k_encode_head(
+    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce,
+    const uint8_t *__restrict__ flags, const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len,
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+    const DevSession *__restrict__ sessions, uint32_t max_sessions, MsgState *__restrict__ state,
+    uint32_t *__restrict__ powtab, unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt,
+    uint32_t *__restrict__ nch_out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
+    const DevSession &ses = sessions[s];
+    uint32_t key[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        key[t] = ses.enc_key[t];
+    const uint64_t nc = nonce[i];
+    const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
+    const uint32_t P = len[i];
+    uint32_t hw[3];
+    const uint32_t hl = plaintext_header(flags[i], ses.downgrade_sub, hw);
+    const uint32_t mlen = hl + P;
+
+    uint32_t ks[16];
+    salsa20_block(ks, key, n0, n1, 0, 0);
+    const fe r = poly_r_from_key(ks[0], ks[1], ks[2], ks[3]);
+
+    // plaintext bytes 0..31 = header || payload[0 .. 32-hl)
+    uint32_t pw[16];
+    load_window(in + in_off[i], P < 32 ? (int) P : 32, pw);
+    uint32_t pt[8];
+    switch (hl) {
+    case 1: shift_in<1>(pw, pt); break;
+    case 2: shift_in<2>(pw, pt); break;
+    case 8: shift_in<8>(pw, pt); break;
+    default: shift_in<11>(pw, pt); break;
+    }
+    pt[0] |= hw[0];
+    pt[1] |= hw[1];
+    pt[2] |= hw[2];
+    const int nv0 = mlen < 32 ? (int) mlen : 32;
+    uint32_t ct[16];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        ct[t] = pt[t] ^ ks[8 + t];
+        ct[8 + t] = 0;
+    }
+    mask_tail(ct, nv0);
+
+    uint8_t *o = out + out_off[i];
+    uint32_t hdr[16] = {0x53454d07u, 0x45474153u, n0, n1};
+    store_window(o, 16, hdr);
+    store_window(o + 32, nv0, ct);
+
+    fe h = fe_zero();
+    const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+    poly_absorb64(h, r, s1, s2, s3, s4, ct, nv0);
+
+    uint32_t nch, blast;
+    body_geometry(mlen, nch, blast);
+    fe rb, hf;
+    head_powers(r, nch, blast, powtab + (size_t) i * kMaxPow * 5, rb, hf);
+    if (mlen > 32)
+        fe_mul(h, hf);
+
+    MsgState st;
+    store_fe(st.r, r);
+    st.nch = nch;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        st.s[t] = ks[4 + t];
+        st.tag[t] = 0;
+    }
+    store_fe(st.hh, h);
+    st.mlen = mlen;
+    store_fe(st.rb, rb);
+    st.hl = hl;
+    st.status = 0;
+    st.flags = 0;
+    st.nonce = nc;
+    st.peer_snap = 0;
+    state[i] = st;
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+        acc[(size_t) i * 5 + t] = 0;
+    cnt[i] = 0;
+    nch_out[i] = nch;
+}
+
+// Segmented (by frame) sum of the lanes' Poly1305 contributions over one
+// wave; returns true on the first lane of each segment, which then holds
+// the segment total.
+__device__ __forceinline__ bool wave_segment_sum(uint32_t key, uint64_t v[5])
+{
+    const int lane = threadIdx.x & 63;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t kd = __shfl_down(key, d);
+        const bool take = (lane + d < 64) && kd == key && key != kIdle;
+        if (!__any(take))
+            break;
+        uint64_t t[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            t[q] = __shfl_down(v[q], d);
+        if (take) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                v[q] += t[q];
+        }
+    }
+    const uint32_t kp = __shfl_up(key, 1);
+    return key != kIdle && (lane == 0 || kp != key);
+}
+
+// Combine a segment total into the frame's accumulator.  Returns true when
+// this call completes the frame; `sum` then holds the frame total.
+__device__ __forceinline__ bool frame_combine(uint32_t g0, uint32_t nch, unsigned long long *acc, uint32_t *cnt,
+                                              uint64_t sum[5])
+{
+    const uint32_t w0 = g0 >> 6, w1 = (g0 + nch - 1) >> 6;
+    if (w0 == w1)
+        return true; // the whole frame is inside this wave's segment
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        __hip_atomic_fetch_add(acc + q, (unsigned long long) sum[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old != w1 - w0)
+        return false;
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        sum[q] = __hip_atomic_load(acc + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// Per-lane contribution factor: r^(Poly1305 blocks after chunk c).
+__device__ __forceinline__ void apply_chunk_factor(fe &x, uint32_t c, uint32_t nch, const fe &rb,
+                                                   const uint32_t *powtab)
+{
+    if (c + 1 >= nch)
+        return;
+    fe_mul(x, rb);
+    const uint32_t m = nch - 2 - c;
+    for (int k = 0; (m >> k) != 0; ++k)
+        if ((m >> k) & 1)
+            fe_mul(x, load_fe(powtab + 5 * k));
+}
+
+__global__ __launch_bounds__(kBodyThreads) void k_encode_body(
+    uint32_t n, const uint32_t *__restrict__ chunk_end, const uint32_t *__restrict__ sid,
+    const uint64_t *__restrict__ nonce, const uint64_t *__restrict__ in_off, const uint8_t *__restrict__ in,
+    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
+    uint32_t max_sessions, const MsgState *__restrict__ state, const uint32_t *__restrict__ powtab,
+    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt)
+{
+    const uint32_t total = chunk_end[n - 1];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
+        const uint32_t g = base + lane;
+        uint32_t key = kIdle;
+        uint64_t v[5] = {0, 0, 0, 0, 0};
+        uint32_t g0 = 0;
+        if (g < total) {
+            const uint32_t i = lower_bound_chunk(chunk_end, n, g);
+            key = i;
+            g0 = i ? chunk_end[i - 1] : 0;
+            const uint32_t c = g - g0;
+            const MsgState &st = state[i];
+            const uint32_t mlen = st.mlen, nch = st.nch, hl = st.hl;
+            const fe r = load_fe(st.r);
+            const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
+            uint32_t k[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                k[t] = sessions[s].enc_key[t];
+            const uint64_t nc = nonce[i];
+            const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
+            const uint8_t *src = in + in_off[i];
+            uint8_t *dst = out + out_off[i] + 32;
+            const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+            fe h = fe_zero();
+            for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t j = 1 + 4 * c + t;
+                const uint32_t pos = 64 * j - 32; // ciphertext byte index
+                if (pos >= mlen)
+                    break;
+                const int nv = mlen - pos >= 64 ? 64 : (int) (mlen - pos);
+                uint32_t ks[16], w[16];
+                salsa20_block(ks, k, n0, n1, j, 0);
+                load_window(src + (pos - hl), nv, w);
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    w[q] ^= ks[q];
+                if (nv < 64)
+                    mask_tail(w, nv);
+                store_window(dst + pos, nv, w);
+                poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+            }
+            apply_chunk_factor(h, c, nch, load_fe(st.rb), powtab + (size_t) i * kMaxPow * 5);
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                v[q] = h.l[q];
+        }
+        if (wave_segment_sum(key, v)) {
+            const uint32_t i = key;
+            const MsgState &st = state[i];
+            if (frame_combine(g0, st.nch, acc + (size_t) i * 5, cnt + i, v)) {
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    v[q] += st.hh[q];
+                const fe tot = fe_from_wide(v);
+                uint32_t tag[16];
+                poly_finish(tot, st.s, tag);
+                store_window(out + out_off[i] + 16, 16, tag);
+            }
+        }
+    }
+}
+
+// =====================================================================
+// decode
+// =====================================================================
+__global__ __launch_bounds__(kHeadThreads) void k_decode_head(
+    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ in_off,
+    const uint32_t *__restrict__ wire_len, const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off,
+    uint8_t *__restrict__ out, const DevSession *__restrict__ sessions, uint32_t max_sessions,
+    const unsigned long long *__restrict__ peer, MsgState *__restrict__ state, uint32_t *__restrict__ powtab,
+    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, uint32_t *__restrict__ nch_out,
+    unsigned long long *__restrict__ vout, uint32_t *__restrict__ iota)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
+    const uint32_t wl = wire_len[i];
+    uint32_t w[16];
+    load_window(in + in_off[i], wl < 64 ? (int) wl : 64, w);
+    const uint32_t b0 = w[0] & 0xff;
+    int32_t status = 0;
+    if (wl <= 1 || wl <= b0)
+        status = ZMQG_ERR_MALFORMED_UNSPECIFIED; // src/mechanism_base.cpp:16-22
+    else if (wl < 8 || w[0] != 0x53454d07u || w[1] != 0x45474153u)
+        status = ZMQG_ERR_UNEXPECTED_COMMAND; // src/curve_mechanism_base.cpp:85-90
+    else if (wl < 33)
+        status = ZMQG_ERR_MALFORMED_MESSAGE; // :92-96
+
+    MsgState st;
+    st.status = status;
+    st.hl = 0;
+    st.peer_snap = peer[s];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        acc[(size_t) i * 5 + t] = 0;
+        st.r[t] = st.hh[t] = st.rb[t] = 0;
+    }
+    cnt[i] = 0;
+    iota[i] = i;
+    if (status != 0) {
+        st.nch = 1;
+        st.mlen = 0;
+        st.flags = 0;
+        st.nonce = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            st.s[t] = st.tag[t] = 0;
+        state[i] = st;
+        nch_out[i] = 1;
+        vout[i] = 0;
+        return;
+    }
+    const uint64_t nc = ((uint64_t) bswap32(w[2]) << 32) | bswap32(w[3]);
+    const uint32_t mlen = wl - 32;
+    uint32_t key[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        key[t] = sessions[s].dec_key[t];
+    uint32_t ks[16];
+    salsa20_block(ks, key, w[2], w[3], 0, 0);
+    const fe r = poly_r_from_key(ks[0], ks[1], ks[2], ks[3]);
+    const int nv0 = mlen < 32 ? (int) mlen : 32;
+    uint32_t ct[16];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        ct[t] = w[8 + t];
+        ct[8 + t] = 0;
+    }
+    fe h = fe_zero();
+    const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+    poly_absorb64(h, r, s1, s2, s3, s4, ct, nv0);
+    uint32_t pt[16];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        pt[t] = ct[t] ^ ks[8 + t];
+        pt[8 + t] = 0;
+    }
+    mask_tail(pt, nv0);
+    // payload bytes 0 .. nv0-2 = plaintext bytes 1 .. nv0-1 (speculative:
+    // zeroed by the finisher if the frame fails)
+    uint32_t pay[16];
+#pragma unroll
+    for (int t = 0; t < 15; ++t)
+        pay[t] = __builtin_amdgcn_alignbyte(pt[t + 1], pt[t], 1);
+    pay[15] = 0;
+    store_window(out + out_off[i], nv0 - 1, pay);
+
+    uint32_t nch, blast;
+    body_geometry(mlen, nch, blast);
+    fe rb, hf;
+    head_powers(r, nch, blast, powtab + (size_t) i * kMaxPow * 5, rb, hf);
+    if (mlen > 32)
+        fe_mul(h, hf);
+    store_fe(st.r, r);
+    st.nch = nch;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        st.s[t] = ks[4 + t];
+        st.tag[t] = w[4 + t];
+    }
+    store_fe(st.hh, h);
+    st.mlen = mlen;
+    store_fe(st.rb, rb);
+    st.flags = pt[0] & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND);
+    st.nonce = nc;
+    state[i] = st;
+    nch_out[i] = nch;
+    vout[i] = nc;
+}
+
+__global__ void k_gather_u64(uint32_t n, const uint32_t *__restrict__ perm, const unsigned long long *__restrict__ src,
+                             unsigned long long *__restrict__ dst)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        dst[i] = src[perm[i]];
+}
+
+__global__ void k_scatter_replay(uint32_t n, const uint32_t *__restrict__ perm, const uint32_t *__restrict__ keys_s,
+                                 const unsigned long long *__restrict__ excl_s, unsigned long long *__restrict__ excl,
+                                 uint8_t *__restrict__ last)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t m = perm[i];
+    excl[m] = excl_s[i];
+    last[m] = (i + 1 == n || keys_s[i + 1] != keys_s[i]) ? 1 : 0;
+}
+
+__global__ void k_last_single(uint32_t n, uint8_t *__restrict__ last)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        last[i] = (i + 1 == n) ? 1 : 0;
+}
+
+__device__ __forceinline__ bool sequence_ok(const MsgState &st, unsigned long long excl)
+{
+    const unsigned long long prev = excl > st.peer_snap ? excl : st.peer_snap;
+    return st.nonce > prev; // src/curve_mechanism_base.cpp:99-104
+}
+
+__global__ __launch_bounds__(kBodyThreads) void k_decode_body(
+    uint32_t n, const uint32_t *__restrict__ chunk_end, const uint32_t *__restrict__ sid,
+    const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ wire_len, const uint8_t *__restrict__ in,
+    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint8_t *__restrict__ flags_out,
+    int32_t *__restrict__ status_out, const DevSession *__restrict__ sessions, uint32_t max_sessions,
+    unsigned long long *__restrict__ peer, const MsgState *__restrict__ state, const uint32_t *__restrict__ powtab,
+    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
+    const unsigned long long *__restrict__ vnon, const uint8_t *__restrict__ last)
+{
+    const uint32_t total = chunk_end[n - 1];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
+        const uint32_t g = base + lane;
+        uint32_t key = kIdle;
+        uint64_t v[5] = {0, 0, 0, 0, 0};
+        uint32_t g0 = 0;
+        if (g < total) {
+            const uint32_t i = lower_bound_chunk(chunk_end, n, g);
+            key = i;
+            g0 = i ? chunk_end[i - 1] : 0;
+            const uint32_t c = g - g0;
+            const MsgState &st = state[i];
+            if (st.status == 0 && sequence_ok(st, excl[i])) {
+                const uint32_t mlen = st.mlen, nch = st.nch;
+                const fe r = load_fe(st.r);
+                const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
+                uint32_t k[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    k[t] = sessions[s].dec_key[t];
+                const uint64_t nc = st.nonce;
+                const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
+                const uint8_t *src = in + in_off[i] + 32; // ciphertext byte 0
+                uint8_t *dst = out + out_off[i];        // payload byte 0 = plaintext byte 1
+                const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+                fe h = fe_zero();
+                for (uint32_t t = 0; t < 4; ++t) {
+                    const uint32_t j = 1 + 4 * c + t;
+                    const uint32_t pos = 64 * j - 32;
+                    if (pos >= mlen)
+                        break;
+                    const int nv = mlen - pos >= 64 ? 64 : (int) (mlen - pos);
+                    uint32_t ks[16], w[16];
+                    salsa20_block(ks, k, n0, n1, j, 0);
+                    load_window(src + pos, nv, w);
+                    poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        w[q] ^= ks[q];
+                    if (nv < 64)
+                        mask_tail(w, nv);
+                    store_window(dst + (pos - 1), nv, w);
+                }
+                apply_chunk_factor(h, c, nch, load_fe(st.rb), powtab + (size_t) i * kMaxPow * 5);
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    v[q] = h.l[q];
+            }
+        }
+        if (wave_segment_sum(key, v)) {
+            const uint32_t i = key;
+            const MsgState &st = state[i];
+            if (frame_combine(g0, st.nch, acc + (size_t) i * 5, cnt + i, v)) {
+                int32_t status = st.status;
+                const unsigned long long ex = excl[i];
+                if (status == 0 && !sequence_ok(st, ex))
+                    status = ZMQG_ERR_INVALID_SEQUENCE;
+                if (status == 0) {
+#pragma unroll
+                    for (int q = 0; q < 5; ++q)
+                        v[q] += st.hh[q];
+                    uint32_t tag[4];
+                    poly_finish(fe_from_wide(v), st.s, tag);
+                    const uint32_t diff = (tag[0] ^ st.tag[0]) | (tag[1] ^ st.tag[1]) | (tag[2] ^ st.tag[2]) |
+                                          (tag[3] ^ st.tag[3]);
+                    if (diff)
+                        status = ZMQG_ERR_CRYPTOGRAPHIC; // :277-281
+                }
+                status_out[i] = status;
+                flags_out[i] = status == 0 ? (uint8_t) st.flags : 0;
+                const uint32_t wl = wire_len[i];
+                if (status != 0 && wl >= 33) {
+                    uint8_t *o = out + out_off[i];
+                    for (uint32_t b = 0; b < wl - 33; ++b)
+                        o[b] = 0;
+                }
+                if (last[i]) {
+                    // _cn_peer_nonce after the batch: max over accepted headers
+                    unsigned long long p = st.peer_snap;
+                    if (ex > p)
+                        p = ex;
+                    if (vnon[i] > p)
+                        p = vnon[i];
+                    peer[sid[i] < max_sessions ? sid[i] : 0] = p;
+                }
+            }
+        }
+    }
+}
+
+} // namespace
+
+// =====================================================================
+// host side
+// =====================================================================
+namespace {
+
+template <typename T>
+int grow(zmqg_ctx *ctx, T *&p, size_t count)
+{
+    if (p)
+        ZCHECK(ctx, hipFree(p));
+    p = nullptr;
+    ZCHECK(ctx, hipMalloc((void **) &p, count * sizeof(T) + 64));
+    return 0;
+}
+
+int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
+{
+    Workspace &w = ctx->ws;
+    if (n > w.cap) {
+        uint64_t cap = w.cap ? w.cap : 1024;
+        while (cap < n)
+            cap *= 2;
+        int rc;
+        if ((rc = grow(ctx, w.state, cap)) || (rc = grow(ctx, w.powtab, cap * kMaxPow * 5)) ||
+            (rc = grow(ctx, w.acc, cap * 5)) || (rc = grow(ctx, w.cnt, cap)) || (rc = grow(ctx, w.nch, cap)) ||
+            (rc = grow(ctx, w.chunk_end, cap)) || (rc = grow(ctx, w.v, cap)) || (rc = grow(ctx, w.excl, cap)) ||
+            (rc = grow(ctx, w.v_s, cap)) || (rc = grow(ctx, w.excl_s, cap)) || (rc = grow(ctx, w.iota, cap)) ||
+            (rc = grow(ctx, w.perm, cap)) || (rc = grow(ctx, w.keys_s, cap)) || (rc = grow(ctx, w.last, cap)))
+            return rc;
+        w.cap = cap;
+    }
+    // hipCUB temporaries for n frames
+    size_t need = 0, b = 0;
+    const int nn = (int) n;
+    ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, b, w.nch, w.chunk_end, nn));
+    need = b > need ? b : need;
+    b = 0;
+    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScan(nullptr, b, w.v, w.excl, hipcub::Max(), 0ull, nn));
+    need = b > need ? b : need;
+    if (ctx->sort_bits > 0) {
+        b = 0;
+        ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t *) nullptr, w.keys_s,
+                                                        (const uint32_t *) nullptr, w.perm, nn, 0, ctx->sort_bits));
+        need = b > need ? b : need;
+        b = 0;
+        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScanByKey(nullptr, b, w.keys_s, w.v_s, w.excl_s, hipcub::Max(),
+                                                            0ull, nn));
+        need = b > need ? b : need;
+    }
+    if (need > w.temp_bytes) {
+        size_t cap = w.temp_bytes ? w.temp_bytes : 4096;
+        while (cap < need)
+            cap *= 2;
+        if (w.temp)
+            ZCHECK(ctx, hipFree(w.temp));
+        w.temp = nullptr;
+        ZCHECK(ctx, hipMalloc(&w.temp, cap));
+        w.temp_bytes = cap;
+    }
+    return 0;
+}
+
+uint32_t body_grid(uint64_t n)
+{
+    // one lane per 256-byte chunk; grid-stride beyond 1024 workgroups
+    // (4 per CU on the 256 CUs of an MI355X).
+    (void) n;
+    return 1024;
+}
+
+int check_n(uint64_t n)
+{
+    return n > 0x7fffffffull ? -EINVAL : 0;
+}
+
+hipEvent_t pool_event(zmqg_ctx *ctx)
+{
+    if (!ctx->event_pool.empty()) {
+        hipEvent_t e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess)
+        return nullptr;
+    return e;
+}
+
+// RAII-free pair recorder: begin() before the launch, end() after.
+struct ProfSpan {
+    zmqg_ctx *ctx;
+    int kind;
+    hipStream_t st;
+    hipEvent_t a = nullptr;
+    ProfSpan(zmqg_ctx *c, int k, hipStream_t s) : ctx(c), kind(k), st(s)
+    {
+        if (ctx->profiling && (a = pool_event(ctx)))
+            (void) hipEventRecord(a, st);
+    }
+    void end()
+    {
+        if (!a)
+            return;
+        hipEvent_t b = pool_event(ctx);
+        if (b) {
+            (void) hipEventRecord(b, st);
+            ctx->prof[kind].push_back({a, b});
+        } else {
+            ctx->event_pool.push_back(a);
+        }
+        a = nullptr;
+    }
+};
+
+} // namespace
+
+extern "C" {
+
+int zmqg_abi_version(void)
+{
+    return ZMQG_CURVE_ABI_VERSION;
+}
+
+int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
+{
+    if (!ctx_out || max_sessions == 0)
+        return -EINVAL;
+    *ctx_out = nullptr;
+    zmqg_ctx *ctx = new (std::nothrow) zmqg_ctx;
+    if (!ctx)
+        return -ENOMEM;
+    ctx->device = device;
+    ctx->max_sessions = max_sessions;
+    int bits = 0;
+    while (bits < 32 && (1ull << bits) < max_sessions)
+        ++bits;
+    ctx->sort_bits = bits;
+    ctx->h_downgrade.assign(max_sessions, 0);
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess)
+        e = hipMalloc((void **) &ctx->sessions, sizeof(DevSession) * max_sessions);
+    if (e == hipSuccess)
+        e = hipMemset(ctx->sessions, 0, sizeof(DevSession) * max_sessions);
+    if (e == hipSuccess)
+        e = hipMalloc((void **) &ctx->peer, sizeof(unsigned long long) * max_sessions);
+    if (e == hipSuccess)
+        e = hipMemset(ctx->peer, 0, sizeof(unsigned long long) * max_sessions);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        zmqg_ctx_destroy(ctx);
+        return -EIO;
+    }
+    *ctx_out = ctx;
+    return 0;
+}
+
+int zmqg_ctx_destroy(zmqg_ctx *ctx)
+{
+    if (!ctx)
+        return -EINVAL;
+    (void) hipSetDevice(ctx->device);
+    (void) hipDeviceSynchronize();
+    Workspace &w = ctx->ws;
+    void *ptrs[] = {w.state, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
+                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
+    for (void *p : ptrs)
+        if (p)
+            (void) hipFree(p);
+    if (ctx->pin)
+        (void) hipHostFree(ctx->pin);
+    if (ctx->own_stream)
+        (void) hipStreamDestroy(ctx->own_stream);
+    for (auto &v : ctx->prof)
+        for (auto &p : v) {
+            (void) hipEventDestroy(p.first);
+            (void) hipEventDestroy(p.second);
+        }
+    for (hipEvent_t e : ctx->event_pool)
+        (void) hipEventDestroy(e);
+    delete ctx;
+    return 0;
+}
+
+int zmqg_ctx_set_profiling(zmqg_ctx *ctx, int enable)
+{
+    if (!ctx)
+        return -EINVAL;
+    ctx->profiling = enable != 0;
+    return 0;
+}
+
+int zmqg_ctx_get_profile(zmqg_ctx *ctx, int kind, double *ms_total, uint64_t *launches)
+{
+    if (!ctx || kind < 0 || kind > 3 || !ms_total || !launches)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    ZCHECK(ctx, hipDeviceSynchronize());
+    double tot = 0;
+    for (auto &p : ctx->prof[kind]) {
+        float ms = 0;
+        ZCHECK(ctx, hipEventElapsedTime(&ms, p.first, p.second));
+        tot += ms;
+        ctx->event_pool.push_back(p.first);
+        ctx->event_pool.push_back(p.second);
+    }
+    *ms_total = tot;
+    *launches = ctx->prof[kind].size();
+    ctx->prof[kind].clear();
+    return 0;
+}
+
+const char *zmqg_last_error(zmqg_ctx *ctx)
+{
+    return ctx ? ctx->last_error : "null ctx";
+}
+
+int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], const uint8_t enc_prefix[16],
+                     const uint8_t dec_prefix[16], int downgrade_sub, uint64_t peer_nonce)
+{
+    if (!ctx || !precom || !enc_prefix || !dec_prefix || sid >= ctx->max_sessions)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    uint32_t in[19];
+    memcpy(in, precom, 32);
+    memcpy(in + 8, enc_prefix, 16);
+    memcpy(in + 12, dec_prefix, 16);
+    in[16] = downgrade_sub ? 1u : 0u;
+    in[17] = (uint32_t) peer_nonce;
+    in[18] = (uint32_t) (peer_nonce >> 32);
+    ctx->h_downgrade[sid] = downgrade_sub ? 1 : 0;
+    uint32_t *d = nullptr;
+    ZCHECK(ctx, hipMalloc((void **) &d, sizeof in));
+    hipError_t e = hipMemcpyAsync(d, in, sizeof in, hipMemcpyHostToDevice, ctx->own_stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_session_setup, dim3(1), dim3(64), 0, ctx->own_stream, ctx->sessions, ctx->peer, sid, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(ctx->own_stream);
+    (void) hipFree(d);
+    ZCHECK(ctx, e);
+    return 0;
+}
+
+int zmqg_session_set_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t peer_nonce)
+{
+    if (!ctx || sid >= ctx->max_sessions)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    ZCHECK(ctx, hipDeviceSynchronize());
+    hipLaunchKernelGGL(k_set_peer, dim3(1), dim3(64), 0, ctx->own_stream, ctx->peer, sid,
+                       (unsigned long long) peer_nonce);
+    ZCHECK(ctx, hipGetLastError());
+    ZCHECK(ctx, hipStreamSynchronize(ctx->own_stream));
+    return 0;
+}
+
+int zmqg_session_get_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *peer_nonce_out)
+{
+    if (!ctx || sid >= ctx->max_sessions || !peer_nonce_out)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    ZCHECK(ctx, hipDeviceSynchronize());
+    unsigned long long v = 0;
+    ZCHECK(ctx, hipMemcpy(&v, ctx->peer + sid, sizeof v, hipMemcpyDeviceToHost));
+    *peer_nonce_out = v;
+    return 0;
+}
+
+uint64_t zmqg_wire_size(uint8_t msg_flags, int downgrade_sub, uint64_t payload_len)
+{
+    const uint32_t ct = msg_flags & 0x1c;
+    uint64_t hl = 1;
+    if (ct == ZMQG_MSG_SUBSCRIBE || ct == ZMQG_MSG_CANCEL)
+        hl = downgrade_sub ? 2 : (ct == ZMQG_MSG_CANCEL ? 8 : 11);
+    return 32 + hl + payload_len;
+}
+
+int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                      const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                      uint8_t *out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!sid || !nonce || !flags || !in_off || !len || !in || !out_off || !out)
+        return -EINVAL;
+    hipStream_t st = (hipStream_t) stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    int rc = ensure_workspace(ctx, n);
+    if (rc)
+        return rc;
+    Workspace &w = ctx->ws;
+    const uint32_t nn = (uint32_t) n;
+    ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
+    hipLaunchKernelGGL(k_encode_head, dim3((nn + kHeadThreads - 1) / kHeadThreads), dim3(kHeadThreads), 0, st, nn,
+                       sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions, ctx->max_sessions, w.state,
+                       w.powtab, w.acc, w.cnt, w.nch);
+    ZCHECK(ctx, hipGetLastError());
+    size_t tb = w.temp_bytes;
+    ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
+    ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
+    hipLaunchKernelGGL(k_encode_body, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid, nonce,
+                       in_off, in, out_off, out, ctx->sessions, ctx->max_sessions, w.state, w.powtab, w.acc, w.cnt);
+    ZCHECK(ctx, hipGetLastError());
+    body.end();
+    call.end();
+    return 0;
+}
+
+int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                      const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
+                      uint8_t *flags_out, int32_t *status_out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!sid || !in_off || !wire_len || !in || !out_off || !out || !flags_out || !status_out)
+        return -EINVAL;
+    hipStream_t st = (hipStream_t) stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    int rc = ensure_workspace(ctx, n);
+    if (rc)
+        return rc;
+    Workspace &w = ctx->ws;
+    const uint32_t nn = (uint32_t) n;
+    const dim3 hgrid((nn + kHeadThreads - 1) / kHeadThreads);
+    ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
+    hipLaunchKernelGGL(k_decode_head, hgrid, dim3(kHeadThreads), 0, st, nn, sid, in_off, wire_len, in, out_off, out,
+                       ctx->sessions, ctx->max_sessions, ctx->peer, w.state, w.powtab, w.acc, w.cnt, w.nch, w.v,
+                       w.iota);
+    ZCHECK(ctx, hipGetLastError());
+    size_t tb = w.temp_bytes;
+    if (ctx->sort_bits == 0) {
+        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScan(w.temp, tb, w.v, w.excl, hipcub::Max(), 0ull, (int) nn, st));
+        hipLaunchKernelGGL(k_last_single, hgrid, dim3(kHeadThreads), 0, st, nn, w.last);
+        ZCHECK(ctx, hipGetLastError());
+    } else {
+        tb = w.temp_bytes;
+        ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(w.temp, tb, sid, w.keys_s, w.iota, w.perm, (int) nn, 0,
+                                                        ctx->sort_bits, st));
+        hipLaunchKernelGGL(k_gather_u64, hgrid, dim3(kHeadThreads), 0, st, nn, w.perm, w.v, w.v_s);
+        ZCHECK(ctx, hipGetLastError());
+        tb = w.temp_bytes;
+        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScanByKey(w.temp, tb, w.keys_s, w.v_s, w.excl_s, hipcub::Max(),
+                                                            0ull, (int) nn, hipcub::Equality(), st));
+        hipLaunchKernelGGL(k_scatter_replay, hgrid, dim3(kHeadThreads), 0, st, nn, w.perm, w.keys_s, w.excl_s, w.excl,
+                           w.last);
+        ZCHECK(ctx, hipGetLastError());
+    }
+    tb = w.temp_bytes;
+    ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
+    ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
+    hipLaunchKernelGGL(k_decode_body, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid, in_off,
+                       wire_len, in, out_off, out, flags_out, status_out, ctx->sessions, ctx->max_sessions, ctx->peer,
+                       w.state, w.powtab, w.acc, w.cnt, w.excl, w.v, w.last);
+    ZCHECK(ctx, hipGetLastError());
+    body.end();
+    call.end();
+    return 0;
+}
+
+// ---------------------------------------------------------------- host forms
+static int stage(zmqg_ctx *ctx, size_t bytes)
+{
+    if (bytes > ctx->pin_bytes) {
+        if (ctx->pin)
+            ZCHECK(ctx, hipHostFree(ctx->pin));
+        ctx->pin = nullptr;
+        ctx->pin_bytes = 0;
+        ZCHECK(ctx, hipHostMalloc((void **) &ctx->pin, bytes));
+        ctx->pin_bytes = bytes;
+    }
+    if (bytes > ctx->dbuf_bytes) {
+        if (ctx->dbuf)
+            ZCHECK(ctx, hipFree(ctx->dbuf));
+        ctx->dbuf = nullptr;
+        ctx->dbuf_bytes = 0;
+        ZCHECK(ctx, hipMalloc((void **) &ctx->dbuf, bytes));
+        ctx->dbuf_bytes = bytes;
+    }
+    return 0;
+}
+
+static size_t al(size_t x)
+{
+    return (x + 255) & ~(size_t) 255;
+}
+
+int zmqg_encode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                     const uint64_t *in_off, const uint32_t *len, const uint8_t *in, uint64_t in_bytes,
+                     const uint64_t *out_off, uint8_t *out, uint64_t out_bytes)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!sid || !nonce || !flags || !in_off || !len || !in || !out_off || !out)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (sid[i] >= ctx->max_sessions || in_off[i] + len[i] > in_bytes)
+            return -EINVAL;
+        if (out_off[i] + zmqg_wire_size(flags[i], ctx->h_downgrade[sid[i]], len[i]) > out_bytes)
+            return -EINVAL;
+    }
+    const size_t o_sid = 0, o_nonce = al(o_sid + 4 * n), o_flags = al(o_nonce + 8 * n), o_inoff = al(o_flags + n),
+                 o_len = al(o_inoff + 8 * n), o_outoff = al(o_len + 4 * n), o_in = al(o_outoff + 8 * n),
+                 o_out = al(o_in + in_bytes), total = al(o_out + out_bytes);
+    int rc = stage(ctx, total);
+    if (rc)
+        return rc;
+    uint8_t *h = ctx->pin, *d = ctx->dbuf;
+    memcpy(h + o_sid, sid, 4 * n);
+    memcpy(h + o_nonce, nonce, 8 * n);
+    memcpy(h + o_flags, flags, n);
+    memcpy(h + o_inoff, in_off, 8 * n);
+    memcpy(h + o_len, len, 4 * n);
+    memcpy(h + o_outoff, out_off, 8 * n);
+    memcpy(h + o_in, in, in_bytes);
+    hipStream_t st = ctx->own_stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    ZCHECK(ctx, hipMemcpyAsync(d, h, o_out, hipMemcpyHostToDevice, st));
+    rc = zmqg_encode_batch(ctx, n, (uint32_t *) (d + o_sid), (uint64_t *) (d + o_nonce), d + o_flags,
+                           (uint64_t *) (d + o_inoff), (uint32_t *) (d + o_len), d + o_in,
+                           (uint64_t *) (d + o_outoff), d + o_out, st);
+    if (rc)
+        return rc;
+    ZCHECK(ctx, hipMemcpyAsync(h + o_out, d + o_out, out_bytes, hipMemcpyDeviceToHost, st));
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    memcpy(out, h + o_out, out_bytes);
+    return 0;
+}
+
+int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                     const uint32_t *wire_len, const uint8_t *in, uint64_t in_bytes, const uint64_t *out_off,
+                     uint8_t *out, uint64_t out_bytes, uint8_t *flags_out, int32_t *status_out)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!sid || !in_off || !wire_len || !in || !out_off || !out || !flags_out || !status_out)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (sid[i] >= ctx->max_sessions || in_off[i] + wire_len[i] > in_bytes)
+            return -EINVAL;
+        if (wire_len[i] >= 33 && out_off[i] + wire_len[i] - 33 > out_bytes)
+            return -EINVAL;
+    }
+    const size_t o_sid = 0, o_inoff = al(o_sid + 4 * n), o_wl = al(o_inoff + 8 * n), o_outoff = al(o_wl + 4 * n),
+                 o_in = al(o_outoff + 8 * n), o_out = al(o_in + in_bytes), o_fl = al(o_out + out_bytes),
+                 o_st = al(o_fl + n), total = al(o_st + 4 * n);
+    int rc = stage(ctx, total);
+    if (rc)
+        return rc;
+    uint8_t *h = ctx->pin, *d = ctx->dbuf;
+    memcpy(h + o_sid, sid, 4 * n);
+    memcpy(h + o_inoff, in_off, 8 * n);
+    memcpy(h + o_wl, wire_len, 4 * n);
+    memcpy(h + o_outoff, out_off, 8 * n);
+    memcpy(h + o_in, in, in_bytes);
+    memcpy(h + o_out, out, out_bytes); // bytes of `out` outside the frames are preserved
+    hipStream_t st = ctx->own_stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    ZCHECK(ctx, hipMemcpyAsync(d, h, o_fl, hipMemcpyHostToDevice, st));
+    rc = zmqg_decode_batch(ctx, n, (uint32_t *) (d + o_sid), (uint64_t *) (d + o_inoff), (uint32_t *) (d + o_wl),
+                           d + o_in, (uint64_t *) (d + o_outoff), d + o_out, d + o_fl, (int32_t *) (d + o_st), st);
+    if (rc)
+        return rc;
+    ZCHECK(ctx, hipMemcpyAsync(h + o_out, d + o_out, total - o_out, hipMemcpyDeviceToHost, st));
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    memcpy(out, h + o_out, out_bytes);
+    memcpy(flags_out, h + o_fl, n);
+    memcpy(status_out, h + o_st, 4 * n);
+    return 0;
+}
+
+} // extern "C"

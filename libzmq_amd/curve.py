@@ -1,0 +1,277 @@
+"""Host-side mirror of libzmq's CURVE message codec over the MI355X C ABI.
+
+Python view of include/zmqg_curve.h (libzmq_amd/libzmqg_curve.so).  Two
+layers:
+
+* ``CurveContext`` -- the batch API: one call encodes or decodes many frames
+  held in device memory (torch tensors on the ctx's device) or host memory.
+* ``CurveEncoding`` -- the single-message interface of the reference's
+  ``curve_encoding_t`` (src/curve_mechanism_base.hpp:26-59): ``encode(msg)``,
+  ``decode(msg) -> (rc, error_event_code)``, ``get_writable_precom_buffer``,
+  ``set_peer_nonce``, ``get_and_inc_nonce``, with the reference's return /
+  errno / error-event conventions (src/curve_mechanism_base.cpp:80-284).
+
+There is no CPU fallback: if the HIP library is missing, importing this module
+raises.  Build it with ``python -c "import __graft_entry__ as g; g.build()"``.
+"""
+import ctypes
+import errno
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzmqg_curve.so")
+
+# include/zmq.h:424-437 (= ZMQG_ERR_* of include/zmqg_curve.h)
+ERR_UNEXPECTED_COMMAND = 0x10000001
+ERR_INVALID_SEQUENCE = 0x10000002
+ERR_MALFORMED_UNSPECIFIED = 0x10000011
+ERR_MALFORMED_MESSAGE = 0x10000012
+ERR_CRYPTOGRAPHIC = 0x11000001
+
+# src/msg.hpp:55-62
+MORE, COMMAND, SUBSCRIBE, CANCEL = 1, 2, 12, 16
+CLIENT_PREFIX = b"CurveZMQMESSAGEC"  # src/curve_client.cpp:22-23
+SERVER_PREFIX = b"CurveZMQMESSAGES"
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: the MI355X CURVE path has no CPU fallback. "
+        "Build it with `make -C libzmq_amd/csrc` (hipcc --offload-arch=gfx950).")
+
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+_U32 = ctypes.c_uint32
+_lib = ctypes.CDLL(LIB_PATH)
+_lib.zmqg_abi_version.restype = ctypes.c_int
+_lib.zmqg_ctx_create.argtypes = [ctypes.c_int, _U32, ctypes.POINTER(_P)]
+_lib.zmqg_ctx_destroy.argtypes = [_P]
+_lib.zmqg_session_set.argtypes = [_P, _U32, _P, _P, _P, ctypes.c_int, _U64]
+_lib.zmqg_session_set_peer_nonce.argtypes = [_P, _U32, _U64]
+_lib.zmqg_session_get_peer_nonce.argtypes = [_P, _U32, ctypes.POINTER(_U64)]
+_lib.zmqg_wire_size.argtypes = [ctypes.c_uint8, ctypes.c_int, _U64]
+_lib.zmqg_wire_size.restype = _U64
+_lib.zmqg_encode_batch.argtypes = [_P, _U64] + [_P] * 9
+_lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
+_lib.zmqg_encode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _U64, _P, _P, _U64]
+_lib.zmqg_decode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _U64, _P, _P, _U64, _P, _P]
+_lib.zmqg_ctx_set_profiling.argtypes = [_P, ctypes.c_int]
+_lib.zmqg_ctx_get_profile.argtypes = [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
+_lib.zmqg_last_error.argtypes = [_P]
+_lib.zmqg_last_error.restype = ctypes.c_char_p
+assert _lib.zmqg_abi_version() == 1
+
+
+def lib():
+    return _lib
+
+
+def wire_size(msg_flags, downgrade_sub, payload_len):
+    """Encoded frame size (src/curve_mechanism_base.cpp:113-128, 169)."""
+    return int(_lib.zmqg_wire_size(msg_flags & 0xFF, int(bool(downgrade_sub)), payload_len))
+
+
+class ZmqgError(RuntimeError):
+    pass
+
+
+def _ptr(x):
+    """Device/host address of a torch tensor or numpy array."""
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        return ctypes.c_void_p(x.ctypes.data)
+    return ctypes.c_void_p(x.data_ptr())
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+class CurveContext:
+    """A zmqg_ctx: a session table on one GPU plus batch encode/decode."""
+
+    def __init__(self, device=0, max_sessions=1):
+        self._ctx = _P()
+        self.device = device
+        self.max_sessions = max_sessions
+        self.downgrade = [False] * max_sessions
+        rc = _lib.zmqg_ctx_create(device, max_sessions, ctypes.byref(self._ctx))
+        if rc != 0:
+            raise ZmqgError(f"zmqg_ctx_create failed: {rc}")
+
+    def close(self):
+        if self._ctx:
+            _lib.zmqg_ctx_destroy(self._ctx)
+            self._ctx = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise ZmqgError(f"{what} failed: {rc} ({_lib.zmqg_last_error(self._ctx).decode()})")
+
+    def session_set(self, sid, precom, enc_prefix, dec_prefix, downgrade_sub=False, peer_nonce=1):
+        precom, enc_prefix, dec_prefix = bytes(precom), bytes(enc_prefix), bytes(dec_prefix)
+        if len(precom) != 32 or len(enc_prefix) != 16 or len(dec_prefix) != 16:
+            raise ValueError("precom must be 32 bytes and prefixes 16 bytes")
+        self.downgrade[sid] = bool(downgrade_sub)
+        self._check(_lib.zmqg_session_set(self._ctx, sid, precom, enc_prefix, dec_prefix, int(bool(downgrade_sub)),
+                                          peer_nonce), "zmqg_session_set")
+
+    def set_peer_nonce(self, sid, nonce):
+        self._check(_lib.zmqg_session_set_peer_nonce(self._ctx, sid, nonce), "zmqg_session_set_peer_nonce")
+
+    def get_peer_nonce(self, sid):
+        v = _U64(0)
+        self._check(_lib.zmqg_session_get_peer_nonce(self._ctx, sid, ctypes.byref(v)), "zmqg_session_get_peer_nonce")
+        return v.value
+
+    # ---- profiling hooks (HIP events around the body kernels) ----
+    PROF_ENCODE_BODY, PROF_DECODE_BODY, PROF_ENCODE_CALL, PROF_DECODE_CALL = 0, 1, 2, 3
+
+    def set_profiling(self, enable):
+        self._check(_lib.zmqg_ctx_set_profiling(self._ctx, int(bool(enable))), "zmqg_ctx_set_profiling")
+
+    def get_profile(self, kind):
+        """(total_ms, launches) for `kind` since the last call; resets."""
+        ms = ctypes.c_double(0)
+        cnt = _U64(0)
+        self._check(_lib.zmqg_ctx_get_profile(self._ctx, kind, ctypes.byref(ms), ctypes.byref(cnt)),
+                    "zmqg_ctx_get_profile")
+        return ms.value, cnt.value
+
+    # ---- device-resident batches (torch tensors on self.device) ----
+    def encode_batch(self, sid, nonce, flags, in_off, length, inp, out_off, out, stream=None):
+        n = int(sid.numel())
+        self._check(_lib.zmqg_encode_batch(self._ctx, n, _ptr(sid), _ptr(nonce), _ptr(flags), _ptr(in_off),
+                                           _ptr(length), _ptr(inp), _ptr(out_off), _ptr(out), _stream_handle(stream)),
+                    "zmqg_encode_batch")
+
+    def decode_batch(self, sid, in_off, wire_len, inp, out_off, out, flags_out, status_out, stream=None):
+        n = int(sid.numel())
+        self._check(_lib.zmqg_decode_batch(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
+                                           _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
+                                           _stream_handle(stream)), "zmqg_decode_batch")
+
+    # ---- host-memory batches (numpy), staged through pinned buffers ----
+    def encode_host(self, sid, nonce, flags, in_off, length, inp, out_off, out_size):
+        sid = np.ascontiguousarray(sid, np.uint32)
+        nonce = np.ascontiguousarray(nonce, np.uint64)
+        flags = np.ascontiguousarray(flags, np.uint8)
+        in_off = np.ascontiguousarray(in_off, np.uint64)
+        length = np.ascontiguousarray(length, np.uint32)
+        inp = np.ascontiguousarray(inp, np.uint8)
+        out_off = np.ascontiguousarray(out_off, np.uint64)
+        out = np.zeros(max(out_size, 1), np.uint8)
+        self._check(_lib.zmqg_encode_host(self._ctx, len(sid), _ptr(sid), _ptr(nonce), _ptr(flags), _ptr(in_off),
+                                          _ptr(length), _ptr(inp), inp.nbytes, _ptr(out_off), _ptr(out), out.nbytes),
+                    "zmqg_encode_host")
+        return out[:out_size]
+
+    def decode_host(self, sid, in_off, wire_len, inp, out_off, out_size):
+        sid = np.ascontiguousarray(sid, np.uint32)
+        in_off = np.ascontiguousarray(in_off, np.uint64)
+        wire_len = np.ascontiguousarray(wire_len, np.uint32)
+        inp = np.ascontiguousarray(inp, np.uint8)
+        out_off = np.ascontiguousarray(out_off, np.uint64)
+        n = len(sid)
+        out = np.zeros(max(out_size, 1), np.uint8)
+        fl = np.zeros(max(n, 1), np.uint8)
+        st = np.zeros(max(n, 1), np.int32)
+        self._check(_lib.zmqg_decode_host(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
+                                          inp.nbytes, _ptr(out_off), _ptr(out), out.nbytes, _ptr(fl), _ptr(st)),
+                    "zmqg_decode_host")
+        return out[:out_size], fl[:n], st[:n]
+
+
+class Msg:
+    """Minimal stand-in for zmq::msg_t on this path: bytes + flags byte
+    (src/msg.hpp:55-62).  ``set_flags`` ORs, as msg_t::set_flags does."""
+
+    def __init__(self, data=b"", flags=0):
+        self.data = bytes(data)
+        self.flags = flags
+
+    def size(self):
+        return len(self.data)
+
+    def set_flags(self, f):
+        self.flags |= f
+
+
+class CurveEncoding:
+    """curve_encoding_t (src/curve_mechanism_base.hpp:26-59) backed by the GPU.
+
+    Each instance owns one session of a shared CurveContext (or its own)."""
+
+    def __init__(self, encode_nonce_prefix, decode_nonce_prefix, downgrade_sub, ctx=None, sid=0):
+        self._enc_prefix = bytes(encode_nonce_prefix)
+        self._dec_prefix = bytes(decode_nonce_prefix)
+        self._downgrade_sub = bool(downgrade_sub)
+        self._ctx = ctx if ctx is not None else CurveContext(0, 1)
+        self._sid = sid
+        self._cn_nonce = 1  # src/curve_mechanism_base.cpp:59-60
+        self._precom = bytearray(32)
+        self._installed = None
+
+    def get_writable_precom_buffer(self):
+        self._installed = None
+        return self._precom
+
+    def _install(self, peer_nonce=None):
+        key = bytes(self._precom)
+        if self._installed != key:
+            cur = 1 if peer_nonce is None else peer_nonce
+            self._ctx.session_set(self._sid, key, self._enc_prefix, self._dec_prefix, self._downgrade_sub, cur)
+            self._installed = key
+
+    def get_and_inc_nonce(self):
+        n = self._cn_nonce
+        self._cn_nonce += 1
+        return n
+
+    def set_peer_nonce(self, nonce):
+        self._install()
+        self._ctx.set_peer_nonce(self._sid, nonce)
+
+    def get_peer_nonce(self):
+        self._install()
+        return self._ctx.get_peer_nonce(self._sid)
+
+    def encode(self, msg):
+        """Replaces msg's content with the MESSAGE frame; returns 0."""
+        self._install()
+        nonce = self.get_and_inc_nonce()
+        payload = np.frombuffer(msg.data, np.uint8) if msg.size() else np.zeros(1, np.uint8)
+        ws = wire_size(msg.flags, self._downgrade_sub, msg.size())
+        out = self._ctx.encode_host([self._sid], [nonce], [msg.flags], [0], [msg.size()], payload, [0], ws)
+        msg.data = out.tobytes()
+        msg.flags = 0  # the encoder output is a fresh msg_t (src/curve_mechanism_base.cpp:167-177)
+        return 0
+
+    def decode(self, msg):
+        """Returns (rc, error_event_code): (0, None) and msg holds the payload
+        with the decoded flags ORed in, or (-1, code) with errno EPROTO."""
+        self._install()
+        wire = np.frombuffer(msg.data, np.uint8) if msg.size() else np.zeros(1, np.uint8)
+        plen = max(msg.size() - 33, 0)
+        out, fl, st = self._ctx.decode_host([self._sid], [0], [msg.size()], wire, [0], plen)
+        if st[0] != 0:
+            return -1, int(st[0])
+        msg.data = out[:plen].tobytes()
+        msg.set_flags(int(fl[0]))
+        return 0, None
+
+
+EPROTO = errno.EPROTO
