@@ -313,9 +313,8 @@ __device__ __forceinline__ void mask_tail(uint32_t w[16], int nv)
 // so the access never leaves the 4-byte granules of the valid range.
 __device__ __forceinline__ void load_window(const uint8_t *p, int nv, uint32_t w[16])
 {
-    const uintptr_t a = (uintptr_t) p;
-    const uint32_t *q = (const uint32_t *) (a & ~(uintptr_t) 3);
-    const uint32_t sh = (uint32_t) (a & 3);
+    const uint32_t sh = (uint32_t) ((uintptr_t) p & 3);
+    const uint32_t *q = (const uint32_t *) (p - sh); // keep the global address space (no inttoptr)
     uint32_t d[17];
     if (nv >= 64) {
 #pragma unroll
@@ -350,6 +349,7 @@ __device__ __forceinline__ void store_window(uint8_t *p, int nv, const uint32_t 
         return;
     }
     const uint32_t s = (4u - sh) & 3u; // bytes before the first aligned dword
+    (void) a;
     uint32_t e[16];
 #pragma unroll
     for (int k = 0; k < 15; ++k)
@@ -364,7 +364,7 @@ __device__ __forceinline__ void store_window(uint8_t *p, int nv, const uint32_t 
         return;
     const int rem = nv - (int) s;
     const int nd = rem >> 2;
-    uint32_t *q = (uint32_t *) (a + s);
+    uint32_t *q = (uint32_t *) (p + s);
 #pragma unroll
     for (int k = 0; k < 16; ++k)
         if (k < nd)

@@ -34,6 +34,10 @@
 #include "../../include/zmqg_curve.h"
 #include "curve_device.hpp"
 
+#ifndef ZMQG_ABLATE
+#define ZMQG_ABLATE 0
+#endif
+
 using namespace zmqg;
 
 namespace {
@@ -470,15 +474,34 @@ __global__ __launch_bounds__(kBodyThreads) void k_encode_body(
                     break;
                 const int nv = mlen - pos >= 64 ? 64 : (int) (mlen - pos);
                 uint32_t ks[16], w[16];
+#if ZMQG_ABLATE == 2 // timing experiment only: memory traffic without keystream/MAC work
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    ks[q] = j * 16 + q;
+#else
                 salsa20_block(ks, k, n0, n1, j, 0);
+#endif
+#if ZMQG_ABLATE == 1 // timing experiment only: keystream/MAC work without memory traffic
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    w[q] = g * 64 + q;
+#else
                 load_window(src + (pos - hl), nv, w);
+#endif
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
                     w[q] ^= ks[q];
                 if (nv < 64)
                     mask_tail(w, nv);
+#if ZMQG_ABLATE == 1
+                if (w[3] == 0x9e3779b9u && w[7] == 0x7f4a7c15u)
+#endif
                 store_window(dst + pos, nv, w);
+#if ZMQG_ABLATE != 2
                 poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+#else
+                h.l[0] ^= w[0];
+#endif
             }
             apply_chunk_factor(h, c, nch, load_fe(st.rb), powtab + (size_t) i * kMaxPow * 5);
 #pragma unroll

@@ -21,7 +21,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzmqg_curve.so")
+LIB_PATH = os.environ.get("ZMQG_CURVE_LIB") or os.path.join(HERE, "libzmqg_curve.so")  # override: experiments
 
 # include/zmq.h:424-437 (= ZMQG_ERR_* of include/zmqg_curve.h)
 ERR_UNEXPECTED_COMMAND = 0x10000001
