@@ -384,4 +384,198 @@ __device__ __forceinline__ void store_window(uint8_t *p, int nv, const uint32_t 
     }
 }
 
+
+// ---------------------------------------------------------------- streams
+// Global-address-space views (keep global_load/store, not flat, for
+// addresses rebuilt from integers).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint8_t GU8;
+typedef __attribute__((address_space(1))) const u32x4 GCU4;
+typedef __attribute__((address_space(1))) u32x4 GU4;
+typedef __attribute__((address_space(1))) uint32_t GU32;
+
+// out[i] = v[i + ws] for a runtime ws in 0..3, branch-free (two cndmask
+// stages), so lanes of differently aligned frames never diverge.
+template <int N>
+__device__ __forceinline__ void select_shift(const uint32_t *v, uint32_t ws, uint32_t *out)
+{
+    // bit-select (v_bfi_b32) rather than ?: so the optimizer cannot turn the
+    // selects back into a dynamically indexed (scratch) array
+    const uint32_t m1 = 0u - (ws & 1u), m2 = 0u - ((ws >> 1) & 1u);
+    uint32_t a[N + 2];
+#pragma unroll
+    for (int i = 0; i < N + 2; ++i)
+        a[i] = (v[i + 1] & m1) | (v[i] & ~m1);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        out[i] = (a[i + 2] & m2) | (a[i] & ~m2);
+}
+
+// Sequential reader of 64-byte windows of a byte stream of L bytes at an
+// arbitrary address.  Loads whole aligned 16-byte granules (dwordx4), each
+// once (one carried between windows), and never a granule with no valid byte.
+struct StreamReader {
+    const GCU4 *g;  // aligned-down base
+    uint32_t off;   // base misalignment (0..15)
+    uint32_t end;   // off + L
+    u32x4 carry;    // granule 4t, loaded with the previous window
+};
+
+__device__ __forceinline__ void reader_init(StreamReader &r, uint64_t p, uint32_t L)
+{
+    r.off = (uint32_t) (p & 15);
+    r.g = (const GCU4 *) (uintptr_t) (p - r.off);
+    r.end = r.off + L;
+    r.carry = (L > 0) ? r.g[0] : (u32x4){0, 0, 0, 0};
+}
+
+__device__ __forceinline__ u32x4 granule_or_zero(const StreamReader &r, uint32_t k)
+{
+    return (16 * k < r.end) ? r.g[k] : (u32x4){0, 0, 0, 0};
+}
+
+// Window t: stream bytes [64t, 64t+64) (valid up to nv), zero beyond nv.
+__device__ __forceinline__ void reader_window(StreamReader &r, uint32_t t, int nv, uint32_t w[16])
+{
+    const u32x4 a = r.carry;
+    const u32x4 b = granule_or_zero(r, 4 * t + 1), c = granule_or_zero(r, 4 * t + 2),
+                d = granule_or_zero(r, 4 * t + 3), e = granule_or_zero(r, 4 * t + 4);
+    r.carry = e;
+    const uint32_t v[20] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y,
+                            c.z, c.w, d.x, d.y, d.z, d.w, e.x, e.y, e.z, e.w};
+    uint32_t u[17];
+    select_shift<17>(v, r.off >> 2, u);
+    const uint32_t bs = r.off & 3;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        w[i] = __builtin_amdgcn_alignbyte(u[i + 1], u[i], bs);
+    if (nv < 64)
+        mask_tail(w, nv);
+}
+
+// Store `len` (< 16) bytes of the 4 words at an aligned address.
+__device__ __forceinline__ void store_partial_granule(GU8 *p, int len, const uint32_t o[4])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rem = len - 4 * k;
+        if (rem >= 4) {
+            *(GU32 *) (p + 4 * k) = o[k];
+        } else if (rem > 0) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (b < rem)
+                    p[4 * k + b] = (uint8_t) (o[k] >> (8 * b));
+        }
+    }
+}
+
+// Writer of a lane's output stream S (L bytes) to an arbitrarily aligned
+// address a.  The s0 bytes before the first 16-byte aligned address are
+// stored individually; the rest goes out as whole aligned granules (dwordx4)
+// once complete, plus at most one partial granule at the end.  Granule G
+// holds stream bytes [s0 + 16G, s0 + 16G + 16).  Windows in order.
+struct GranuleWriter {
+    uint64_t a;  // stream byte 0
+    uint32_t s0; // 0..15
+    int L;
+    uint32_t p12, p13, p14, p15; // previous window's last words
+};
+
+__device__ __forceinline__ void gw_init(GranuleWriter &gw, uint64_t a, int L)
+{
+    gw.a = a;
+    gw.s0 = (16u - (uint32_t) (a & 15)) & 15u;
+    gw.L = L;
+    gw.p12 = gw.p13 = gw.p14 = gw.p15 = 0;
+}
+
+__device__ __forceinline__ void gw_window(GranuleWriter &gw, int t, const uint32_t w[16])
+{
+    GU8 *base = (GU8 *) (uintptr_t) gw.a;
+    GU8 *gq = base + gw.s0; // first aligned granule
+    if (t == 0) { // the s0 leading bytes (inside words 0..3)
+        const int lead = (int) gw.s0 < gw.L ? (int) gw.s0 : gw.L;
+#pragma unroll
+        for (int b = 0; b < 15; ++b)
+            if (b < lead)
+                base[b] = (uint8_t) (w[b >> 2] >> (8 * (b & 3)));
+    }
+    // v = stream words 16t-4 .. 16t+19 (previous tail, this window, zeros)
+    const uint32_t v[24] = {gw.p12, gw.p13, gw.p14, gw.p15, w[0], w[1], w[2],  w[3],  w[4],  w[5],  w[6], w[7],
+                            w[8],   w[9],   w[10],  w[11],  w[12], w[13], w[14], w[15], 0u,    0u,    0u,   0u};
+    uint32_t u[21];
+    select_shift<21>(v, gw.s0 >> 2, u);
+    const uint32_t bs = gw.s0 & 3;
+    const bool last = gw.L <= 64 * t + 64;
+    // candidate granules G = 4t-1+q; a granule is emitted in the window
+    // that completes it, or in the last window if the stream ends inside it
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const int G = 4 * t - 1 + q;
+        const int start = (int) gw.s0 + 16 * G;
+        const int endg = start + 16;
+        const bool due = (endg > 64 * t && endg <= 64 * t + 64) || (last && endg > 64 * t + 64);
+        const int len = gw.L - start;
+        if (!due || G < 0 || len <= 0)
+            continue;
+        const uint32_t o[4] = {__builtin_amdgcn_alignbyte(u[4 * q + 1], u[4 * q], bs),
+                               __builtin_amdgcn_alignbyte(u[4 * q + 2], u[4 * q + 1], bs),
+                               __builtin_amdgcn_alignbyte(u[4 * q + 3], u[4 * q + 2], bs),
+                               __builtin_amdgcn_alignbyte(u[4 * q + 4], u[4 * q + 3], bs)};
+        if (len >= 16)
+            *(GU4 *) (gq + 16 * G) = (u32x4){o[0], o[1], o[2], o[3]};
+        else
+            store_partial_granule(gq + 16 * G, len, o);
+    }
+    gw.p12 = w[12];
+    gw.p13 = w[13];
+    gw.p14 = w[14];
+    gw.p15 = w[15];
+}
+
+// ---------------------------------------------------------------- wave search
+// For the wave's chunk window [g0, g0+64): returns in every lane the frame
+// index of chunk g (first i with chunk_end[i] > g), by a 64-ary search for
+// the window's first frame (each lane tests one probe per round) and a
+// 6-step search over the <= 64 frames the window can touch.
+__device__ __forceinline__ uint32_t wave_find_frame(const uint32_t *__restrict__ chunk_end, uint32_t n, uint32_t g0,
+                                                    uint32_t g)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t lo = 0, hi = n; // answer in [lo, hi]
+    while (hi - lo > 64) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t probe = lo + lane * step;
+        const bool p = probe < hi && chunk_end[probe] > g0;
+        const unsigned long long m = __ballot(p);
+        if (m == 0) { // every probe below hi failed: answer is above the last one
+            const uint32_t k = (hi - 1 - lo) / step;
+            lo = lo + (k < 63 ? k : 63) * step + 1;
+        } else {
+            const uint32_t f = __builtin_ctzll(m);
+            const uint32_t nhi = lo + f * step;
+            lo = f ? lo + (f - 1) * step + 1 : lo;
+            hi = nhi;
+        }
+    }
+    {
+        const uint32_t probe = lo + lane;
+        const bool p = probe < hi && chunk_end[probe] > g0;
+        const unsigned long long m = __ballot(p);
+        lo = m ? lo + (uint32_t) __builtin_ctzll(m) : hi;
+    }
+    // frames lo .. lo+63 cover the window (each frame has >= 1 chunk)
+    const uint32_t mine = lo + lane;
+    const uint32_t ce = mine < n ? chunk_end[mine] : 0xffffffffu;
+    uint32_t a = 0; // first lane index j with ce_j > g
+#pragma unroll
+    for (int b = 32; b >= 1; b >>= 1) {
+        const uint32_t v = __shfl(ce, (int) (a + b - 1));
+        if (v <= g)
+            a += b;
+    }
+    return lo + a;
+}
+
 } // namespace zmqg

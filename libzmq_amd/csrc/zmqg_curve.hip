@@ -241,20 +241,6 @@ __device__ __forceinline__ void shift_in(const uint32_t p[16], uint32_t out[8])
     }
 }
 
-__device__ __forceinline__ uint32_t lower_bound_chunk(const uint32_t *chunk_end, uint32_t n, uint32_t g)
-{
-    // first i with chunk_end[i] > g
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (chunk_end[mid] > g)
-            hi = mid;
-        else
-            lo = mid + 1;
-    }
-    return lo;
-}
-
 // =====================================================================
 // session setup
 // =====================================================================
@@ -433,97 +419,6 @@ __device__ __forceinline__ void apply_chunk_factor(fe &x, uint32_t c, uint32_t n
             fe_mul(x, load_fe(powtab + 5 * k));
 }
 
-__global__ __launch_bounds__(kBodyThreads) void k_encode_body(
-    uint32_t n, const uint32_t *__restrict__ chunk_end, const uint32_t *__restrict__ sid,
-    const uint64_t *__restrict__ nonce, const uint64_t *__restrict__ in_off, const uint8_t *__restrict__ in,
-    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
-    uint32_t max_sessions, const MsgState *__restrict__ state, const uint32_t *__restrict__ powtab,
-    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt)
-{
-    const uint32_t total = chunk_end[n - 1];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
-        const uint32_t g = base + lane;
-        uint32_t key = kIdle;
-        uint64_t v[5] = {0, 0, 0, 0, 0};
-        uint32_t g0 = 0;
-        if (g < total) {
-            const uint32_t i = lower_bound_chunk(chunk_end, n, g);
-            key = i;
-            g0 = i ? chunk_end[i - 1] : 0;
-            const uint32_t c = g - g0;
-            const MsgState &st = state[i];
-            const uint32_t mlen = st.mlen, nch = st.nch, hl = st.hl;
-            const fe r = load_fe(st.r);
-            const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
-            uint32_t k[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-                k[t] = sessions[s].enc_key[t];
-            const uint64_t nc = nonce[i];
-            const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
-            const uint8_t *src = in + in_off[i];
-            uint8_t *dst = out + out_off[i] + 32;
-            const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
-            fe h = fe_zero();
-            for (uint32_t t = 0; t < 4; ++t) {
-                const uint32_t j = 1 + 4 * c + t;
-                const uint32_t pos = 64 * j - 32; // ciphertext byte index
-                if (pos >= mlen)
-                    break;
-                const int nv = mlen - pos >= 64 ? 64 : (int) (mlen - pos);
-                uint32_t ks[16], w[16];
-#if ZMQG_ABLATE == 2 // timing experiment only: memory traffic without keystream/MAC work
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    ks[q] = j * 16 + q;
-#else
-                salsa20_block(ks, k, n0, n1, j, 0);
-#endif
-#if ZMQG_ABLATE == 1 // timing experiment only: keystream/MAC work without memory traffic
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    w[q] = g * 64 + q;
-#else
-                load_window(src + (pos - hl), nv, w);
-#endif
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    w[q] ^= ks[q];
-                if (nv < 64)
-                    mask_tail(w, nv);
-#if ZMQG_ABLATE == 1
-                if (w[3] == 0x9e3779b9u && w[7] == 0x7f4a7c15u)
-#endif
-                store_window(dst + pos, nv, w);
-#if ZMQG_ABLATE != 2
-                poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
-#else
-                h.l[0] ^= w[0];
-#endif
-            }
-            apply_chunk_factor(h, c, nch, load_fe(st.rb), powtab + (size_t) i * kMaxPow * 5);
-#pragma unroll
-            for (int q = 0; q < 5; ++q)
-                v[q] = h.l[q];
-        }
-        if (wave_segment_sum(key, v)) {
-            const uint32_t i = key;
-            const MsgState &st = state[i];
-            if (frame_combine(g0, st.nch, acc + (size_t) i * 5, cnt + i, v)) {
-#pragma unroll
-                for (int q = 0; q < 5; ++q)
-                    v[q] += st.hh[q];
-                const fe tot = fe_from_wide(v);
-                uint32_t tag[16];
-                poly_finish(tot, st.s, tag);
-                store_window(out + out_off[i] + 16, 16, tag);
-            }
-        }
-    }
-}
-
 // =====================================================================
 // decode
 // =====================================================================
@@ -666,101 +561,138 @@ __device__ __forceinline__ bool sequence_ok(const MsgState &st, unsigned long lo
     return st.nonce > prev; // src/curve_mechanism_base.cpp:99-104
 }
 
-__global__ __launch_bounds__(kBodyThreads) void k_decode_body(
+// Body kernel: one lane per chunk (up to 4 Salsa20 blocks = 256 stream
+// bytes).  Each lane streams its chunk with aligned 16-byte loads/stores
+// (StreamReader / GranuleWriter), so arbitrary frame offsets cost a few
+// register shifts, never divergence.
+template <bool DEC>
+__global__ __launch_bounds__(kBodyThreads) void k_body(
     uint32_t n, const uint32_t *__restrict__ chunk_end, const uint32_t *__restrict__ sid,
-    const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ wire_len, const uint8_t *__restrict__ in,
-    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint8_t *__restrict__ flags_out,
-    int32_t *__restrict__ status_out, const DevSession *__restrict__ sessions, uint32_t max_sessions,
-    unsigned long long *__restrict__ peer, const MsgState *__restrict__ state, const uint32_t *__restrict__ powtab,
-    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
-    const unsigned long long *__restrict__ vnon, const uint8_t *__restrict__ last)
+    const uint64_t *__restrict__ nonce, const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ wire_len,
+    const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+    uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out, const DevSession *__restrict__ sessions,
+    uint32_t max_sessions, unsigned long long *__restrict__ peer, const MsgState *__restrict__ state,
+    const uint32_t *__restrict__ powtab, unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt,
+    const unsigned long long *__restrict__ excl, const unsigned long long *__restrict__ vnon,
+    const uint8_t *__restrict__ last)
 {
-    const uint32_t total = chunk_end[n - 1];
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t total = chunk_end[n - 1];
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
         const uint32_t g = base + lane;
-        uint32_t key = kIdle;
+        const uint32_t iw = wave_find_frame(chunk_end, n, base, g);
+        uint32_t key = kIdle, g0 = 0;
         uint64_t v[5] = {0, 0, 0, 0, 0};
-        uint32_t g0 = 0;
         if (g < total) {
-            const uint32_t i = lower_bound_chunk(chunk_end, n, g);
+            const uint32_t i = iw;
             key = i;
             g0 = i ? chunk_end[i - 1] : 0;
             const uint32_t c = g - g0;
             const MsgState &st = state[i];
-            if (st.status == 0 && sequence_ok(st, excl[i])) {
-                const uint32_t mlen = st.mlen, nch = st.nch;
+            const uint32_t mlen = st.mlen;
+            const uint32_t P0 = 32 + 256 * c; // first plaintext byte of this chunk
+            uint32_t L = mlen > P0 ? (mlen - P0 < 256 ? mlen - P0 : 256) : 0;
+            if (DEC && (st.status != 0 || !sequence_ok(st, excl[i])))
+                L = 0;
+            if (L > 0) {
                 const fe r = load_fe(st.r);
                 const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
-                uint32_t k[8];
+                uint32_t kk[8];
 #pragma unroll
                 for (int t = 0; t < 8; ++t)
-                    k[t] = sessions[s].dec_key[t];
-                const uint64_t nc = st.nonce;
+                    kk[t] = DEC ? sessions[s].dec_key[t] : sessions[s].enc_key[t];
+                const uint64_t nc = DEC ? st.nonce : nonce[i];
                 const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
-                const uint8_t *src = in + in_off[i] + 32; // ciphertext byte 0
-                uint8_t *dst = out + out_off[i];        // payload byte 0 = plaintext byte 1
+                StreamReader rd;
+                GranuleWriter gw;
+                if (DEC) {
+                    reader_init(rd, (uint64_t) (uintptr_t) (in + in_off[i] + 32 + P0), L); // ciphertext byte P0
+                    gw_init(gw, (uint64_t) (uintptr_t) (out + out_off[i] + P0 - 1), (int) L); // payload P0-1
+                } else {
+                    reader_init(rd, (uint64_t) (uintptr_t) (in + in_off[i] + (P0 - st.hl)), L); // payload
+                    gw_init(gw, (uint64_t) (uintptr_t) (out + out_off[i] + 32 + P0), (int) L);   // wire ct
+                }
                 const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
                 fe h = fe_zero();
                 for (uint32_t t = 0; t < 4; ++t) {
-                    const uint32_t j = 1 + 4 * c + t;
-                    const uint32_t pos = 64 * j - 32;
-                    if (pos >= mlen)
+                    if (64 * t >= L)
                         break;
-                    const int nv = mlen - pos >= 64 ? 64 : (int) (mlen - pos);
-                    uint32_t ks[16], w[16];
-                    salsa20_block(ks, k, n0, n1, j, 0);
-                    load_window(src + pos, nv, w);
-                    poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+                    const int nv = L - 64 * t >= 64 ? 64 : (int) (L - 64 * t);
+                    uint32_t w[16], ks[16];
+                    reader_window(rd, t, nv, w);
+#if ZMQG_ABLATE == 2 // timing experiment only: memory traffic without keystream/MAC work
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        ks[q] = t * 16 + q;
+#else
+                    salsa20_block(ks, kk, n0, n1, 1 + 4 * c + t, 0);
+#endif
+                    if (DEC && ZMQG_ABLATE != 2)
+                        poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
 #pragma unroll
                     for (int q = 0; q < 16; ++q)
                         w[q] ^= ks[q];
                     if (nv < 64)
                         mask_tail(w, nv);
-                    store_window(dst + (pos - 1), nv, w);
+                    if (!DEC && ZMQG_ABLATE != 2)
+                        poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+#if ZMQG_ABLATE == 2
+                    h.l[0] ^= w[0];
+#endif
+                    gw_window(gw, (int) t, w);
                 }
-                apply_chunk_factor(h, c, nch, load_fe(st.rb), powtab + (size_t) i * kMaxPow * 5);
+                apply_chunk_factor(h, c, st.nch, load_fe(st.rb), powtab + (size_t) i * kMaxPow * 5);
 #pragma unroll
                 for (int q = 0; q < 5; ++q)
                     v[q] = h.l[q];
             }
         }
+        // ---- Poly1305 combine and tag
         if (wave_segment_sum(key, v)) {
             const uint32_t i = key;
             const MsgState &st = state[i];
             if (frame_combine(g0, st.nch, acc + (size_t) i * 5, cnt + i, v)) {
-                int32_t status = st.status;
-                const unsigned long long ex = excl[i];
-                if (status == 0 && !sequence_ok(st, ex))
-                    status = ZMQG_ERR_INVALID_SEQUENCE;
-                if (status == 0) {
+                if (!DEC) {
 #pragma unroll
                     for (int q = 0; q < 5; ++q)
                         v[q] += st.hh[q];
-                    uint32_t tag[4];
+                    uint32_t tag[16];
                     poly_finish(fe_from_wide(v), st.s, tag);
-                    const uint32_t diff = (tag[0] ^ st.tag[0]) | (tag[1] ^ st.tag[1]) | (tag[2] ^ st.tag[2]) |
-                                          (tag[3] ^ st.tag[3]);
-                    if (diff)
-                        status = ZMQG_ERR_CRYPTOGRAPHIC; // :277-281
-                }
-                status_out[i] = status;
-                flags_out[i] = status == 0 ? (uint8_t) st.flags : 0;
-                const uint32_t wl = wire_len[i];
-                if (status != 0 && wl >= 33) {
-                    uint8_t *o = out + out_off[i];
-                    for (uint32_t b = 0; b < wl - 33; ++b)
-                        o[b] = 0;
-                }
-                if (last[i]) {
-                    // _cn_peer_nonce after the batch: max over accepted headers
-                    unsigned long long p = st.peer_snap;
-                    if (ex > p)
-                        p = ex;
-                    if (vnon[i] > p)
-                        p = vnon[i];
-                    peer[sid[i] < max_sessions ? sid[i] : 0] = p;
+                    store_window(out + out_off[i] + 16, 16, tag);
+                } else {
+                    int32_t status = st.status;
+                    const unsigned long long ex = excl[i];
+                    if (status == 0 && !sequence_ok(st, ex))
+                        status = ZMQG_ERR_INVALID_SEQUENCE;
+                    if (status == 0) {
+#pragma unroll
+                        for (int q = 0; q < 5; ++q)
+                            v[q] += st.hh[q];
+                        uint32_t tag[4];
+                        poly_finish(fe_from_wide(v), st.s, tag);
+                        const uint32_t diff = (tag[0] ^ st.tag[0]) | (tag[1] ^ st.tag[1]) | (tag[2] ^ st.tag[2]) |
+                                              (tag[3] ^ st.tag[3]);
+                        if (diff)
+                            status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
+                    }
+                    status_out[i] = status;
+                    flags_out[i] = status == 0 ? (uint8_t) st.flags : 0;
+                    const uint32_t wl = wire_len[i];
+                    if (status != 0 && wl >= 33) {
+                        uint8_t *o = out + out_off[i];
+                        for (uint32_t b = 0; b < wl - 33; ++b)
+                            o[b] = 0;
+                    }
+                    if (last[i]) {
+                        // _cn_peer_nonce after the batch: max over accepted headers
+                        unsigned long long p = st.peer_snap;
+                        if (ex > p)
+                            p = ex;
+                        if (vnon[i] > p)
+                            p = vnon[i];
+                        peer[sid[i] < max_sessions ? sid[i] : 0] = p;
+                    }
                 }
             }
         }
@@ -833,8 +765,8 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
 
 uint32_t body_grid(uint64_t n)
 {
-    // one lane per 256-byte chunk; grid-stride beyond 1024 workgroups
-    // (4 per CU on the 256 CUs of an MI355X).
+    // one lane per 256-byte chunk; 4 workgroups of 4 waves per CU on the
+    // 256 CUs of an MI355X (4 waves per SIMD), grid-stride beyond.
     (void) n;
     return 1024;
 }
@@ -1074,8 +1006,11 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     size_t tb = w.temp_bytes;
     ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
     ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
-    hipLaunchKernelGGL(k_encode_body, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid, nonce,
-                       in_off, in, out_off, out, ctx->sessions, ctx->max_sessions, w.state, w.powtab, w.acc, w.cnt);
+    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid, nonce,
+                       in_off, (const uint32_t *) nullptr, in, out_off, out, (uint8_t *) nullptr, (int32_t *) nullptr,
+                       ctx->sessions, ctx->max_sessions, ctx->peer, w.state, w.powtab, w.acc, w.cnt,
+                       (const unsigned long long *) nullptr, (const unsigned long long *) nullptr,
+                       (const uint8_t *) nullptr);
     ZCHECK(ctx, hipGetLastError());
     body.end();
     call.end();
@@ -1126,9 +1061,10 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     tb = w.temp_bytes;
     ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
     ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
-    hipLaunchKernelGGL(k_decode_body, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid, in_off,
-                       wire_len, in, out_off, out, flags_out, status_out, ctx->sessions, ctx->max_sessions, ctx->peer,
-                       w.state, w.powtab, w.acc, w.cnt, w.excl, w.v, w.last);
+    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid,
+                       (const uint64_t *) nullptr, in_off, wire_len, in, out_off, out, flags_out, status_out,
+                       ctx->sessions, ctx->max_sessions, ctx->peer, w.state, w.powtab, w.acc, w.cnt, w.excl, w.v,
+                       w.last);
     ZCHECK(ctx, hipGetLastError());
     body.end();
     call.end();
