@@ -44,7 +44,7 @@ namespace {
 
 constexpr int kMaxPow = 24;           // r^(16*2^k), k < 24: frames up to 2^32 bytes
 constexpr uint32_t kIdle = 0xffffffffu;
-constexpr int kBodyThreads = 256;
+constexpr int kBodyThreads = 256; // 4 waves x 18.5 KiB LDS staging: 2 workgroups per CU
 constexpr int kHeadThreads = 256;
 
 struct DevSession {
@@ -54,27 +54,46 @@ struct DevSession {
     uint32_t pad[7];
 };
 
-// Per-frame state written by the head kernel, read by the body kernel.
-struct __attribute__((aligned(16))) MsgState {
-    uint32_t r[5];  // Poly1305 r (clamped), 26-bit limbs
-    uint32_t nch;   // body chunks (>= 1; a frame with no body bytes gets one empty chunk)
-    uint32_t s[4];  // Poly1305 pad
-    uint32_t hh[5]; // head blocks' Horner value times r^(body blocks)
-    uint32_t mlen;  // boxed plaintext length (flags + sub/cancel + payload)
-    uint32_t rb[5]; // r^(Poly1305 blocks in the last chunk)
-    uint32_t hl;    // encode: plaintext header length (1, 2, 8 or 11)
-    int32_t status; // decode: header status (0 = header ok)
-    uint32_t flags; // decode: plaintext flags & 3
-    uint32_t tag[4];   // decode: tag carried on the wire
-    uint64_t nonce;    // decode: wire nonce
+// Per-frame records written by the head kernel and read by the body kernel,
+// grouped by when a body lane needs them so each group is one batch of
+// independent dwordx4 loads (no dependent-load chains in the body).
+struct __attribute__((aligned(16))) FrameHot { // needed to start a chunk (96 B)
+    uint32_t key[8];  // XSalsa20 subkey of the frame's session/direction
+    uint32_t r[5];    // Poly1305 r (clamped), 26-bit limbs
+    uint32_t nch;     // body chunks (>= 1; a frame with no body bytes gets one empty chunk)
+    uint32_t mlen;    // boxed plaintext length (flags + sub/cancel + payload)
+    uint32_t hl;      // encode: plaintext header length (1, 2, 8 or 11)
+    uint32_t n0, n1;  // Salsa20 nonce words (the 8 wire nonce bytes, little-endian)
+    int32_t status;   // decode: header status (0 = header ok)
+    uint32_t flags;   // decode: plaintext flags & 3
+    uint64_t in_base;  // encode: payload byte 0; decode: wire byte 0
+    uint64_t out_base; // encode: wire byte 0; decode: payload byte 0
+};
+static_assert(sizeof(FrameHot) == 96, "FrameHot layout");
+
+constexpr int kPowInline = 4; // r^(16*2^k) for k < 4 kept in the record (frames up to 17 chunks)
+struct __attribute__((aligned(16))) FramePow { // chunk factor inputs (112 B)
+    uint32_t rb[5];                // r^(Poly1305 blocks in the last chunk)
+    uint32_t t[kPowInline][5];     // r^(16*2^k)
+    uint32_t pad[3];
+};
+static_assert(sizeof(FramePow) == 112, "FramePow layout");
+
+struct __attribute__((aligned(16))) FrameFin { // tag / status inputs (64 B)
+    uint32_t hh[5];     // head blocks' Horner value times r^(body blocks)
+    uint32_t s[4];      // Poly1305 pad
+    uint32_t tag[4];    // decode: tag carried on the wire
+    uint32_t wire_len;  // decode: frame bytes on the wire
     uint64_t peer_snap; // decode: session peer nonce before this batch
 };
-static_assert(sizeof(MsgState) == 128, "MsgState layout");
+static_assert(sizeof(FrameFin) == 64, "FrameFin layout");
 
 struct Workspace {
     uint64_t cap = 0; // frames
-    MsgState *state = nullptr;
-    uint32_t *powtab = nullptr;   // [cap][kMaxPow][5]
+    FrameHot *hot = nullptr;
+    FramePow *pw = nullptr;
+    FrameFin *fin = nullptr;
+    uint32_t *powtab = nullptr;   // [cap][kMaxPow][5], entries k >= kPowInline
     unsigned long long *acc = nullptr; // [cap][5]
     uint32_t *cnt = nullptr;      // [cap]
     uint32_t *nch = nullptr;      // [cap]
@@ -160,9 +179,10 @@ __device__ __forceinline__ void body_geometry(uint32_t mlen, uint32_t &nch, uint
     blast = (lastb + 15) / 16;
 }
 
-// Computes and stores r^(16*2^k) for k < bits(nch-1), r^blast, and returns
-// the head factor r^(body blocks) = r^blast * (r^16)^(nch-1).
-__device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, uint32_t *powtab, fe &rb, fe &head_factor)
+// Computes r^blast and r^(16*2^k) for k < bits(nch-1) (the first kPowInline
+// into the frame record, the rest into powtab), and returns the head factor
+// r^(body blocks) = r^blast * (r^16)^(nch-1).
+__device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, FramePow *P, uint32_t *powtab, fe &head_factor)
 {
     fe r2 = r;
     fe_mul(r2, r);
@@ -172,7 +192,7 @@ __device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, uint32_t 
     fe_mul(r8, r4);
     fe r16 = r8;
     fe_mul(r16, r8);
-    rb = fe_one();
+    fe rb = fe_one();
     if (blast == 16) {
         rb = r16;
     } else {
@@ -185,20 +205,24 @@ __device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, uint32_t 
         if (blast & 8)
             fe_mul(rb, r8);
     }
+    store_fe(P->rb, rb);
+#pragma unroll
+    for (int k = 0; k < kPowInline; ++k)
+        store_fe(P->t[k], fe_zero());
     head_factor = rb;
-    uint32_t m = nch - 1; // head multiplies by (r^16)^(nch-1)
+    const uint32_t m = nch - 1; // head multiplies by (r^16)^(nch-1)
     fe t = r16;
-    int k = 0;
-    while ((m >> k) != 0) {
-        store_fe(powtab + 5 * k, t);
+    for (int k = 0; (m >> k) != 0; ++k) {
+        if (k < kPowInline)
+            store_fe(P->t[k], t); // global record: a runtime index is fine here
+        else
+            store_fe(powtab + 5 * k, t);
         if ((m >> k) & 1)
             fe_mul(head_factor, t);
         fe t2 = t;
         fe_mul(t2, t);
         t = t2;
-        ++k;
     }
-    // body chunk 0 needs bits of nch-2 < nch-1: already covered.
 }
 
 // plaintext header of src/curve_mechanism_base.cpp:118-158 as 3 words
@@ -275,19 +299,19 @@ __global__ __launch_bounds__(kHeadThreads) void k_encode_head(
     uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce,
     const uint8_t *__restrict__ flags, const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len,
     const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
-    const DevSession *__restrict__ sessions, uint32_t max_sessions, MsgState *__restrict__ state,
-    uint32_t *__restrict__ powtab, unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt,
-    uint32_t *__restrict__ nch_out)
+    const DevSession *__restrict__ sessions, uint32_t max_sessions, FrameHot *__restrict__ hot,
+    FramePow *__restrict__ pw, FrameFin *__restrict__ fin, uint32_t *__restrict__ powtab,
+    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, uint32_t *__restrict__ nch_out)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
         return;
     const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
     const DevSession &ses = sessions[s];
-    uint32_t key[8];
+    FrameHot H;
 #pragma unroll
     for (int t = 0; t < 8; ++t)
-        key[t] = ses.enc_key[t];
+        H.key[t] = ses.enc_key[t];
     const uint64_t nc = nonce[i];
     const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
     const uint32_t P = len[i];
@@ -296,18 +320,19 @@ __global__ __launch_bounds__(kHeadThreads) void k_encode_head(
     const uint32_t mlen = hl + P;
 
     uint32_t ks[16];
-    salsa20_block(ks, key, n0, n1, 0, 0);
+    salsa20_block(ks, H.key, n0, n1, 0, 0);
     const fe r = poly_r_from_key(ks[0], ks[1], ks[2], ks[3]);
 
     // plaintext bytes 0..31 = header || payload[0 .. 32-hl)
-    uint32_t pw[16];
-    load_window(in + in_off[i], P < 32 ? (int) P : 32, pw);
+    const uint8_t *src = in + in_off[i];
+    uint32_t pw16[16];
+    load_window(src, P < 32 ? (int) P : 32, pw16);
     uint32_t pt[8];
     switch (hl) {
-    case 1: shift_in<1>(pw, pt); break;
-    case 2: shift_in<2>(pw, pt); break;
-    case 8: shift_in<8>(pw, pt); break;
-    default: shift_in<11>(pw, pt); break;
+    case 1: shift_in<1>(pw16, pt); break;
+    case 2: shift_in<2>(pw16, pt); break;
+    case 8: shift_in<8>(pw16, pt); break;
+    default: shift_in<11>(pw16, pt); break;
     }
     pt[0] |= hw[0];
     pt[1] |= hw[1];
@@ -332,28 +357,32 @@ __global__ __launch_bounds__(kHeadThreads) void k_encode_head(
 
     uint32_t nch, blast;
     body_geometry(mlen, nch, blast);
-    fe rb, hf;
-    head_powers(r, nch, blast, powtab + (size_t) i * kMaxPow * 5, rb, hf);
+    fe hf;
+    head_powers(r, nch, blast, pw + i, powtab + (size_t) i * kMaxPow * 5, hf);
     if (mlen > 32)
         fe_mul(h, hf);
 
-    MsgState st;
-    store_fe(st.r, r);
-    st.nch = nch;
+    store_fe(H.r, r);
+    H.nch = nch;
+    H.mlen = mlen;
+    H.hl = hl;
+    H.n0 = n0;
+    H.n1 = n1;
+    H.status = 0;
+    H.flags = 0;
+    H.in_base = (uint64_t) (uintptr_t) src;
+    H.out_base = (uint64_t) (uintptr_t) o;
+    hot[i] = H;
+    FrameFin F;
+    store_fe(F.hh, h);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        st.s[t] = ks[4 + t];
-        st.tag[t] = 0;
+        F.s[t] = ks[4 + t];
+        F.tag[t] = 0;
     }
-    store_fe(st.hh, h);
-    st.mlen = mlen;
-    store_fe(st.rb, rb);
-    st.hl = hl;
-    st.status = 0;
-    st.flags = 0;
-    st.nonce = nc;
-    st.peer_snap = 0;
-    state[i] = st;
+    F.wire_len = mlen + 32;
+    F.peer_snap = 0;
+    fin[i] = F;
 #pragma unroll
     for (int t = 0; t < 5; ++t)
         acc[(size_t) i * 5 + t] = 0;
@@ -406,17 +435,22 @@ __device__ __forceinline__ bool frame_combine(uint32_t g0, uint32_t nch, unsigne
     return true;
 }
 
-// Per-lane contribution factor: r^(Poly1305 blocks after chunk c).
-__device__ __forceinline__ void apply_chunk_factor(fe &x, uint32_t c, uint32_t nch, const fe &rb,
-                                                   const uint32_t *powtab)
+// Per-chunk contribution factor r^(Poly1305 blocks after chunk c)
+// = r^blast * (r^16)^(nch-2-c); 1 for the last chunk.
+__device__ __forceinline__ fe chunk_factor(uint32_t c, uint32_t nch, const FramePow &P, const uint32_t *powtab)
 {
     if (c + 1 >= nch)
-        return;
-    fe_mul(x, rb);
+        return fe_one();
+    fe f = load_fe(P.rb);
     const uint32_t m = nch - 2 - c;
-    for (int k = 0; (m >> k) != 0; ++k)
+#pragma unroll
+    for (int k = 0; k < kPowInline; ++k)
         if ((m >> k) & 1)
-            fe_mul(x, load_fe(powtab + 5 * k));
+            fe_mul(f, load_fe(P.t[k]));
+    for (int k = kPowInline; (m >> k) != 0; ++k)
+        if ((m >> k) & 1)
+            fe_mul(f, load_fe(powtab + 5 * k));
+    return f;
 }
 
 // =====================================================================
@@ -426,17 +460,20 @@ __global__ __launch_bounds__(kHeadThreads) void k_decode_head(
     uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ in_off,
     const uint32_t *__restrict__ wire_len, const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off,
     uint8_t *__restrict__ out, const DevSession *__restrict__ sessions, uint32_t max_sessions,
-    const unsigned long long *__restrict__ peer, MsgState *__restrict__ state, uint32_t *__restrict__ powtab,
-    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, uint32_t *__restrict__ nch_out,
-    unsigned long long *__restrict__ vout, uint32_t *__restrict__ iota)
+    const unsigned long long *__restrict__ peer, FrameHot *__restrict__ hot, FramePow *__restrict__ pw,
+    FrameFin *__restrict__ fin, uint32_t *__restrict__ powtab, unsigned long long *__restrict__ acc,
+    uint32_t *__restrict__ cnt, uint32_t *__restrict__ nch_out, unsigned long long *__restrict__ vout,
+    uint32_t *__restrict__ iota, uint8_t *__restrict__ last_single)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
         return;
     const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
     const uint32_t wl = wire_len[i];
+    const uint8_t *src = in + in_off[i];
+    uint8_t *dst = out + out_off[i];
     uint32_t w[16];
-    load_window(in + in_off[i], wl < 64 ? (int) wl : 64, w);
+    load_window(src, wl < 64 ? (int) wl : 64, w);
     const uint32_t b0 = w[0] & 0xff;
     int32_t status = 0;
     if (wl <= 1 || wl <= b0)
@@ -446,38 +483,52 @@ __global__ __launch_bounds__(kHeadThreads) void k_decode_head(
     else if (wl < 33)
         status = ZMQG_ERR_MALFORMED_MESSAGE; // :92-96
 
-    MsgState st;
-    st.status = status;
-    st.hl = 0;
-    st.peer_snap = peer[s];
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
+    for (int t = 0; t < 5; ++t)
         acc[(size_t) i * 5 + t] = 0;
-        st.r[t] = st.hh[t] = st.rb[t] = 0;
-    }
     cnt[i] = 0;
     iota[i] = i;
+    if (last_single)
+        last_single[i] = (i + 1 == n) ? 1 : 0;
+
+    FrameHot H;
+    FrameFin F;
+    F.wire_len = wl;
+    F.peer_snap = peer[s];
+    H.status = status;
+    H.hl = 0;
+    H.in_base = (uint64_t) (uintptr_t) src;
+    H.out_base = (uint64_t) (uintptr_t) dst;
     if (status != 0) {
-        st.nch = 1;
-        st.mlen = 0;
-        st.flags = 0;
-        st.nonce = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            H.key[t] = 0;
+        store_fe(H.r, fe_zero());
+        H.nch = 1;
+        H.mlen = 0;
+        H.n0 = H.n1 = 0;
+        H.flags = 0;
+        store_fe(pw[i].rb, fe_zero());
+#pragma unroll
+        for (int k = 0; k < kPowInline; ++k)
+            store_fe(pw[i].t[k], fe_zero());
+        store_fe(F.hh, fe_zero());
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-            st.s[t] = st.tag[t] = 0;
-        state[i] = st;
+            F.s[t] = F.tag[t] = 0;
+        hot[i] = H;
+        fin[i] = F;
         nch_out[i] = 1;
         vout[i] = 0;
         return;
     }
     const uint64_t nc = ((uint64_t) bswap32(w[2]) << 32) | bswap32(w[3]);
     const uint32_t mlen = wl - 32;
-    uint32_t key[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t)
-        key[t] = sessions[s].dec_key[t];
+        H.key[t] = sessions[s].dec_key[t];
     uint32_t ks[16];
-    salsa20_block(ks, key, w[2], w[3], 0, 0);
+    salsa20_block(ks, H.key, w[2], w[3], 0, 0);
     const fe r = poly_r_from_key(ks[0], ks[1], ks[2], ks[3]);
     const int nv0 = mlen < 32 ? (int) mlen : 32;
     uint32_t ct[16];
@@ -503,27 +554,28 @@ __global__ __launch_bounds__(kHeadThreads) void k_decode_head(
     for (int t = 0; t < 15; ++t)
         pay[t] = __builtin_amdgcn_alignbyte(pt[t + 1], pt[t], 1);
     pay[15] = 0;
-    store_window(out + out_off[i], nv0 - 1, pay);
+    store_window(dst, nv0 - 1, pay);
 
     uint32_t nch, blast;
     body_geometry(mlen, nch, blast);
-    fe rb, hf;
-    head_powers(r, nch, blast, powtab + (size_t) i * kMaxPow * 5, rb, hf);
+    fe hf;
+    head_powers(r, nch, blast, pw + i, powtab + (size_t) i * kMaxPow * 5, hf);
     if (mlen > 32)
         fe_mul(h, hf);
-    store_fe(st.r, r);
-    st.nch = nch;
+    store_fe(H.r, r);
+    H.nch = nch;
+    H.mlen = mlen;
+    H.n0 = w[2];
+    H.n1 = w[3];
+    H.flags = pt[0] & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND);
+    store_fe(F.hh, h);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        st.s[t] = ks[4 + t];
-        st.tag[t] = w[4 + t];
+        F.s[t] = ks[4 + t];
+        F.tag[t] = w[4 + t];
     }
-    store_fe(st.hh, h);
-    st.mlen = mlen;
-    store_fe(st.rb, rb);
-    st.flags = pt[0] & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND);
-    st.nonce = nc;
-    state[i] = st;
+    hot[i] = H;
+    fin[i] = F;
     nch_out[i] = nch;
     vout[i] = nc;
 }
@@ -548,155 +600,313 @@ __global__ void k_scatter_replay(uint32_t n, const uint32_t *__restrict__ perm, 
     last[m] = (i + 1 == n || keys_s[i + 1] != keys_s[i]) ? 1 : 0;
 }
 
-__global__ void k_last_single(uint32_t n, uint8_t *__restrict__ last)
-{
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n)
-        last[i] = (i + 1 == n) ? 1 : 0;
-}
 
-__device__ __forceinline__ bool sequence_ok(const MsgState &st, unsigned long long excl)
+// src/curve_mechanism_base.cpp:99-104: the wire nonce must exceed the peer
+// nonce, which (batch order) is the max of the session's prior value and
+// every earlier header-valid nonce of the session in this batch.
+__device__ __forceinline__ bool sequence_ok(uint64_t nonce, unsigned long long peer_snap, unsigned long long excl)
 {
-    const unsigned long long prev = excl > st.peer_snap ? excl : st.peer_snap;
-    return st.nonce > prev; // src/curve_mechanism_base.cpp:99-104
+    const unsigned long long prev = excl > peer_snap ? excl : peer_snap;
+    return nonce > prev;
 }
 
 // Body kernel: one lane per chunk (up to 4 Salsa20 blocks = 256 stream
 // bytes).  Each lane streams its chunk with aligned 16-byte loads/stores
 // (StreamReader / GranuleWriter), so arbitrary frame offsets cost a few
 // register shifts, never divergence.
+// ---------------------------------------------------------------- body
+// One lane per chunk (up to 4 Salsa20 blocks = 256 stream bytes).  The
+// wave's 64 chunks are staged through LDS so that every global access is a
+// coalesced, aligned 16-byte granule stream (a chunk's granules go to
+// consecutive lanes), which keeps HBM/L2 traffic at the algorithmic bytes:
+//   1. LDS-DMA (global_load_lds_dwordx4): input granule q of chunk s lands
+//      at slot s + 16q, slot = 272 bytes (17 granules), lane-linear.
+//   2. each lane works on its own slot: stream byte b is at slot + (src&15)
+//      + b; the output image (stream byte b at slot + (dst&15) + b) is
+//      written in place, one window behind the input it has already read.
+//   3. interior output granules go back with coalesced dwordx4 stores;
+//      each lane then stores its own (at most two) edge granules, merging
+//      the granule it shares with the next chunk of the same frame.
+constexpr int kSlot = 272;
+struct ChunkParam {
+    uint64_t src; // input stream byte 0 (global address)
+    uint64_t dst; // output stream byte 0 (global address)
+    uint32_t L;   // stream bytes of this chunk (0 = none)
+    uint32_t cont; // the next lane holds the next 256 bytes of the same frame
+};
+static_assert(sizeof(ChunkParam) == 24, "ChunkParam");
+constexpr int kWaveLds = 64 * kSlot + 64 * (int) sizeof(ChunkParam); // 18944 B
+constexpr int kBodyWaves = kBodyThreads / 64;
+
+typedef __attribute__((address_space(3))) void LdsVoid;
+typedef __attribute__((address_space(1))) void GVoid;
+
+__device__ __forceinline__ void wave_lds_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// bytes [lo, hi) of granule v at the 16-byte aligned address p
+__device__ __forceinline__ void store_granule_range(GU8 *p, int lo, int hi, const u32x4 &v)
+{
+    const uint32_t o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int a = lo > 4 * k ? lo : 4 * k;
+        const int b = hi < 4 * k + 4 ? hi : 4 * k + 4;
+        if (a == 4 * k && b == 4 * k + 4) {
+            *(GU32 *) (p + 4 * k) = o[k];
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (4 * k + t >= a && 4 * k + t < b)
+                    p[4 * k + t] = (uint8_t) (o[k] >> (8 * t));
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t byte_mask_below(int e, int k) // bytes [4k, 4k+4) below e
+{
+    const int b = e - 4 * k;
+    return b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+}
+
 template <bool DEC>
 __global__ __launch_bounds__(kBodyThreads) void k_body(
-    uint32_t n, const uint32_t *__restrict__ chunk_end, const uint32_t *__restrict__ sid,
-    const uint64_t *__restrict__ nonce, const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ wire_len,
-    const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
-    uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out, const DevSession *__restrict__ sessions,
-    uint32_t max_sessions, unsigned long long *__restrict__ peer, const MsgState *__restrict__ state,
-    const uint32_t *__restrict__ powtab, unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt,
-    const unsigned long long *__restrict__ excl, const unsigned long long *__restrict__ vnon,
+    uint32_t n, const uint32_t *__restrict__ chunk_end, const FrameHot *__restrict__ hot,
+    const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin, const uint32_t *__restrict__ powtab,
+    uint8_t *__restrict__ out_tag, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
+    const uint32_t *__restrict__ sid, uint32_t max_sessions, unsigned long long *__restrict__ peer,
+    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
     const uint8_t *__restrict__ last)
 {
-    const uint32_t lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * kWaveLds];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t *slots = lds + wv * kWaveLds;
+    ChunkParam *prm = (ChunkParam *) (slots + 64 * kSlot);
+    uint8_t *myslot = slots + lane * kSlot;
     const uint32_t total = chunk_end[n - 1];
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
         const uint32_t g = base + lane;
         const uint32_t iw = wave_find_frame(chunk_end, n, base, g);
-        uint32_t key = kIdle, g0 = 0;
-        uint64_t v[5] = {0, 0, 0, 0, 0};
+        uint32_t key = kIdle, g0 = 0, c = 0, L = 0;
+        uint64_t src = 0, dst = 0;
+        FrameHot H;
+        fe f = fe_one();
         if (g < total) {
             const uint32_t i = iw;
             key = i;
             g0 = i ? chunk_end[i - 1] : 0;
-            const uint32_t c = g - g0;
-            const MsgState &st = state[i];
-            const uint32_t mlen = st.mlen;
+            c = g - g0;
+            H = hot[i];
+            const FramePow Pw = pw[i];
+            unsigned long long ex = 0, psnap = 0;
+            if (DEC) {
+                ex = excl[i];
+                psnap = fin[i].peer_snap;
+            }
             const uint32_t P0 = 32 + 256 * c; // first plaintext byte of this chunk
-            uint32_t L = mlen > P0 ? (mlen - P0 < 256 ? mlen - P0 : 256) : 0;
-            if (DEC && (st.status != 0 || !sequence_ok(st, excl[i])))
-                L = 0;
-            if (L > 0) {
-                const fe r = load_fe(st.r);
-                const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
-                uint32_t kk[8];
+            L = H.mlen > P0 ? (H.mlen - P0 < 256 ? H.mlen - P0 : 256) : 0;
+            if (DEC) {
+                const uint64_t nc = ((uint64_t) bswap32(H.n0) << 32) | bswap32(H.n1);
+                if (H.status != 0 || !sequence_ok(nc, psnap, ex))
+                    L = 0;
+                src = H.in_base + 32 + P0;  // ciphertext byte P0 on the wire
+                dst = H.out_base + P0 - 1;  // plaintext byte P0 = payload byte P0-1
+            } else {
+                src = H.in_base + (P0 - H.hl); // payload byte = plaintext byte - hl
+                dst = H.out_base + 32 + P0;    // wire ciphertext
+            }
+            if (L > 0)
+                f = chunk_factor(c, H.nch, Pw, powtab + (size_t) i * kMaxPow * 5);
+        }
+        const uint32_t kn = __shfl_down(key, 1), Ln = __shfl_down(L, 1);
+        const bool cont = lane < 63 && key != kIdle && kn == key && L == 256 && Ln > 0;
+        const bool prevcont = __shfl_up(cont ? 1u : 0u, 1) != 0 && lane > 0;
+        {
+            ChunkParam p;
+            p.src = src;
+            p.dst = dst;
+            p.L = L;
+            p.cont = cont ? 1u : 0u;
+            prm[lane] = p;
+        }
+        wave_lds_fence();
+        // ---- 1. coalesced LDS-DMA of the input images
+#pragma unroll 1
+        for (uint32_t k = 0; k < 17; ++k) {
+            const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
+            const uint64_t ps = prm[s].src;
+            const uint32_t pL = prm[s].L;
+            const uint32_t off = (uint32_t) (ps & 15);
+            if (pL && q < ((off + pL + 15) >> 4))
+                __builtin_amdgcn_global_load_lds((GVoid *) (uintptr_t) ((ps - off) + 16 * q),
+                                                 (LdsVoid *) (slots + 1024 * k), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_lds_fence();
+        // ---- 2. keystream, MAC, output image (in place, one window behind)
+        uint64_t v[5] = {0, 0, 0, 0, 0};
+        if (L > 0) {
+            const fe r = load_fe(H.r);
+            const uint32_t di = (uint32_t) (src & 15), dO = (uint32_t) (dst & 15);
+            const uint32_t *inw = (const uint32_t *) (myslot + (di & ~3u));
+            uint32_t *outw = (uint32_t *) (myslot + (dO & ~3u));
+            const uint32_t si = di & 3, so = dO & 3;
+            const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+            const uint32_t nwin = (L + 63) >> 6;
+            fe h = fe_zero();
+            uint32_t d[17];
 #pragma unroll
-                for (int t = 0; t < 8; ++t)
-                    kk[t] = DEC ? sessions[s].dec_key[t] : sessions[s].enc_key[t];
-                const uint64_t nc = DEC ? st.nonce : nonce[i];
-                const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
-                StreamReader rd;
-                GranuleWriter gw;
-                if (DEC) {
-                    reader_init(rd, (uint64_t) (uintptr_t) (in + in_off[i] + 32 + P0), L); // ciphertext byte P0
-                    gw_init(gw, (uint64_t) (uintptr_t) (out + out_off[i] + P0 - 1), (int) L); // payload P0-1
-                } else {
-                    reader_init(rd, (uint64_t) (uintptr_t) (in + in_off[i] + (P0 - st.hl)), L); // payload
-                    gw_init(gw, (uint64_t) (uintptr_t) (out + out_off[i] + 32 + P0), (int) L);   // wire ct
+            for (int q = 0; q < 17; ++q)
+                d[q] = inw[q];
+            uint32_t carry = 0;
+            for (uint32_t t = 0; t < nwin; ++t) {
+                const int nv = L - 64 * t >= 64 ? 64 : (int) (L - 64 * t);
+                uint32_t w[16], ks[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    w[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], si);
+                if (t + 1 < nwin) { // read ahead before this window's output overwrites it
+#pragma unroll
+                    for (int q = 0; q < 17; ++q)
+                        d[q] = inw[16 * (t + 1) + q];
                 }
-                const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
-                fe h = fe_zero();
-                for (uint32_t t = 0; t < 4; ++t) {
-                    if (64 * t >= L)
-                        break;
-                    const int nv = L - 64 * t >= 64 ? 64 : (int) (L - 64 * t);
-                    uint32_t w[16], ks[16];
-                    reader_window(rd, t, nv, w);
+                if (nv < 64)
+                    mask_tail(w, nv);
 #if ZMQG_ABLATE == 2 // timing experiment only: memory traffic without keystream/MAC work
 #pragma unroll
-                    for (int q = 0; q < 16; ++q)
-                        ks[q] = t * 16 + q;
+                for (int q = 0; q < 16; ++q)
+                    ks[q] = t * 16 + q;
 #else
-                    salsa20_block(ks, kk, n0, n1, 1 + 4 * c + t, 0);
+                salsa20_block(ks, H.key, H.n0, H.n1, 1 + 4 * c + t, 0);
 #endif
-                    if (DEC && ZMQG_ABLATE != 2)
-                        poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+                if (DEC && ZMQG_ABLATE != 2)
+                    poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    w[q] ^= ks[q];
+                if (nv < 64)
+                    mask_tail(w, nv);
+                if (!DEC && ZMQG_ABLATE != 2)
+                    poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+#if ZMQG_ABLATE == 2
+                h.l[0] ^= w[0];
+#endif
+                // image dword (dO>>2) + 16t + q holds stream bytes [64t + 4q - so, +4)
+                if (so == 0) {
 #pragma unroll
                     for (int q = 0; q < 16; ++q)
-                        w[q] ^= ks[q];
-                    if (nv < 64)
-                        mask_tail(w, nv);
-                    if (!DEC && ZMQG_ABLATE != 2)
-                        poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
-#if ZMQG_ABLATE == 2
-                    h.l[0] ^= w[0];
-#endif
-                    gw_window(gw, (int) t, w);
-                }
-                apply_chunk_factor(h, c, st.nch, load_fe(st.rb), powtab + (size_t) i * kMaxPow * 5);
+                        outw[16 * t + q] = w[q];
+                } else {
+                    outw[16 * t] = __builtin_amdgcn_alignbyte(w[0], carry, 4 - so);
 #pragma unroll
-                for (int q = 0; q < 5; ++q)
-                    v[q] = h.l[q];
+                    for (int q = 1; q < 16; ++q)
+                        outw[16 * t + q] = __builtin_amdgcn_alignbyte(w[q], w[q - 1], 4 - so);
+                    carry = w[15];
+                    if (t + 1 == nwin)
+                        outw[16 * t + 16] = __builtin_amdgcn_alignbyte(0u, w[15], 4 - so);
+                }
+            }
+            fe_mul(h, f);
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                v[q] = h.l[q];
+        }
+        wave_lds_fence();
+        // ---- 3a. coalesced stores of the interior output granules
+#pragma unroll 1
+        for (uint32_t k = 0; k < 17; ++k) {
+            const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
+            const uint64_t pd = prm[s].dst;
+            const uint32_t pL = prm[s].L;
+            const uint32_t dO = (uint32_t) (pd & 15);
+            const uint32_t qfirst = dO ? 1u : 0u;          // granule 0 is an edge when misaligned
+            if (pL && q >= qfirst && 16 * q + 16 <= dO + pL) // whole granule inside the chunk
+                *(GU4 *) (uintptr_t) ((pd - dO) + 16 * q) = *(const u32x4 *) (slots + 16 * idx);
+        }
+        // ---- 3b. this lane's edge granules
+        if (L > 0) {
+            const uint32_t dO = (uint32_t) (dst & 15), end = dO + L;
+            GU8 *gbase = (GU8 *) (uintptr_t) (dst - dO);
+            const uint32_t ql = end >> 4, el = end & 15; // granule of the last byte / its valid bytes
+            if (dO && !prevcont) { // front edge [dO, min(16, end)) (merged by the previous chunk otherwise)
+                const u32x4 gv = *(const u32x4 *) myslot;
+                store_granule_range(gbase, (int) dO, end < 16 ? (int) end : 16, gv);
+            }
+            if (el && (ql >= 1 || dO == 0)) { // back edge [0, el) (granule 0 with dO > 0 was the front edge)
+                u32x4 gv = *(const u32x4 *) (myslot + 16 * ql);
+                int hi = (int) el;
+                if (cont) { // the next chunk's bytes [el, el + L_next) complete it
+                    const u32x4 nx = *(const u32x4 *) (myslot + kSlot);
+                    const int hn = (int) el + (int) Ln;
+                    const uint32_t m0 = byte_mask_below(hi, 0), m1 = byte_mask_below(hi, 1),
+                                   m2 = byte_mask_below(hi, 2), m3 = byte_mask_below(hi, 3);
+                    gv.x = (gv.x & m0) | (nx.x & ~m0);
+                    gv.y = (gv.y & m1) | (nx.y & ~m1);
+                    gv.z = (gv.z & m2) | (nx.z & ~m2);
+                    gv.w = (gv.w & m3) | (nx.w & ~m3);
+                    hi = hn < 16 ? hn : 16;
+                }
+                if (hi == 16)
+                    *(GU4 *) (gbase + 16 * ql) = gv;
+                else
+                    store_granule_range(gbase + 16 * ql, 0, hi, gv);
             }
         }
+        wave_lds_fence();
         // ---- Poly1305 combine and tag
         if (wave_segment_sum(key, v)) {
             const uint32_t i = key;
-            const MsgState &st = state[i];
-            if (frame_combine(g0, st.nch, acc + (size_t) i * 5, cnt + i, v)) {
+            const FrameHot &H = hot[i];
+            if (frame_combine(g0, H.nch, acc + (size_t) i * 5, cnt + i, v)) {
+                const FrameFin F = fin[i];
                 if (!DEC) {
 #pragma unroll
                     for (int q = 0; q < 5; ++q)
-                        v[q] += st.hh[q];
+                        v[q] += F.hh[q];
                     uint32_t tag[16];
-                    poly_finish(fe_from_wide(v), st.s, tag);
-                    store_window(out + out_off[i] + 16, 16, tag);
+                    poly_finish(fe_from_wide(v), F.s, tag);
+                    store_window((uint8_t *) (uintptr_t) H.out_base + 16, 16, tag);
                 } else {
-                    int32_t status = st.status;
+                    int32_t status = H.status;
                     const unsigned long long ex = excl[i];
-                    if (status == 0 && !sequence_ok(st, ex))
+                    const uint64_t nc = ((uint64_t) bswap32(H.n0) << 32) | bswap32(H.n1);
+                    if (status == 0 && !sequence_ok(nc, F.peer_snap, ex))
                         status = ZMQG_ERR_INVALID_SEQUENCE;
                     if (status == 0) {
 #pragma unroll
                         for (int q = 0; q < 5; ++q)
-                            v[q] += st.hh[q];
+                            v[q] += F.hh[q];
                         uint32_t tag[4];
-                        poly_finish(fe_from_wide(v), st.s, tag);
-                        const uint32_t diff = (tag[0] ^ st.tag[0]) | (tag[1] ^ st.tag[1]) | (tag[2] ^ st.tag[2]) |
-                                              (tag[3] ^ st.tag[3]);
+                        poly_finish(fe_from_wide(v), F.s, tag);
+                        const uint32_t diff =
+                            (tag[0] ^ F.tag[0]) | (tag[1] ^ F.tag[1]) | (tag[2] ^ F.tag[2]) | (tag[3] ^ F.tag[3]);
                         if (diff)
                             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
                     }
                     status_out[i] = status;
-                    flags_out[i] = status == 0 ? (uint8_t) st.flags : 0;
-                    const uint32_t wl = wire_len[i];
-                    if (status != 0 && wl >= 33) {
-                        uint8_t *o = out + out_off[i];
-                        for (uint32_t b = 0; b < wl - 33; ++b)
+                    flags_out[i] = status == 0 ? (uint8_t) H.flags : 0;
+                    if (status != 0 && F.wire_len >= 33) {
+                        uint8_t *o = (uint8_t *) (uintptr_t) H.out_base;
+                        for (uint32_t b = 0; b < F.wire_len - 33; ++b)
                             o[b] = 0;
                     }
                     if (last[i]) {
                         // _cn_peer_nonce after the batch: max over accepted headers
-                        unsigned long long p = st.peer_snap;
+                        unsigned long long p = F.peer_snap;
                         if (ex > p)
                             p = ex;
-                        if (vnon[i] > p)
-                            p = vnon[i];
+                        if (H.status == 0 && nc > p)
+                            p = nc;
                         peer[sid[i] < max_sessions ? sid[i] : 0] = p;
                     }
                 }
             }
         }
     }
+    (void) out_tag;
 }
 
 } // namespace
@@ -724,7 +934,8 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
         while (cap < n)
             cap *= 2;
         int rc;
-        if ((rc = grow(ctx, w.state, cap)) || (rc = grow(ctx, w.powtab, cap * kMaxPow * 5)) ||
+        if ((rc = grow(ctx, w.hot, cap)) || (rc = grow(ctx, w.pw, cap)) || (rc = grow(ctx, w.fin, cap)) ||
+            (rc = grow(ctx, w.powtab, cap * kMaxPow * 5)) ||
             (rc = grow(ctx, w.acc, cap * 5)) || (rc = grow(ctx, w.cnt, cap)) || (rc = grow(ctx, w.nch, cap)) ||
             (rc = grow(ctx, w.chunk_end, cap)) || (rc = grow(ctx, w.v, cap)) || (rc = grow(ctx, w.excl, cap)) ||
             (rc = grow(ctx, w.v_s, cap)) || (rc = grow(ctx, w.excl_s, cap)) || (rc = grow(ctx, w.iota, cap)) ||
@@ -865,7 +1076,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     (void) hipSetDevice(ctx->device);
     (void) hipDeviceSynchronize();
     Workspace &w = ctx->ws;
-    void *ptrs[] = {w.state, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
+    void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
                     w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
@@ -1000,17 +1211,15 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     const uint32_t nn = (uint32_t) n;
     ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
     hipLaunchKernelGGL(k_encode_head, dim3((nn + kHeadThreads - 1) / kHeadThreads), dim3(kHeadThreads), 0, st, nn,
-                       sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions, ctx->max_sessions, w.state,
-                       w.powtab, w.acc, w.cnt, w.nch);
+                       sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions, ctx->max_sessions, w.hot,
+                       w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch);
     ZCHECK(ctx, hipGetLastError());
     size_t tb = w.temp_bytes;
     ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
     ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
-    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid, nonce,
-                       in_off, (const uint32_t *) nullptr, in, out_off, out, (uint8_t *) nullptr, (int32_t *) nullptr,
-                       ctx->sessions, ctx->max_sessions, ctx->peer, w.state, w.powtab, w.acc, w.cnt,
-                       (const unsigned long long *) nullptr, (const unsigned long long *) nullptr,
-                       (const uint8_t *) nullptr);
+    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
+                       w.fin, w.powtab, out, (uint8_t *) nullptr, (int32_t *) nullptr, sid, ctx->max_sessions,
+                       ctx->peer, w.acc, w.cnt, (const unsigned long long *) nullptr, (const uint8_t *) nullptr);
     ZCHECK(ctx, hipGetLastError());
     body.end();
     call.end();
@@ -1037,14 +1246,12 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     const dim3 hgrid((nn + kHeadThreads - 1) / kHeadThreads);
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
     hipLaunchKernelGGL(k_decode_head, hgrid, dim3(kHeadThreads), 0, st, nn, sid, in_off, wire_len, in, out_off, out,
-                       ctx->sessions, ctx->max_sessions, ctx->peer, w.state, w.powtab, w.acc, w.cnt, w.nch, w.v,
-                       w.iota);
+                       ctx->sessions, ctx->max_sessions, ctx->peer, w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch,
+                       w.v, w.iota, ctx->sort_bits == 0 ? w.last : (uint8_t *) nullptr);
     ZCHECK(ctx, hipGetLastError());
     size_t tb = w.temp_bytes;
     if (ctx->sort_bits == 0) {
         ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScan(w.temp, tb, w.v, w.excl, hipcub::Max(), 0ull, (int) nn, st));
-        hipLaunchKernelGGL(k_last_single, hgrid, dim3(kHeadThreads), 0, st, nn, w.last);
-        ZCHECK(ctx, hipGetLastError());
     } else {
         tb = w.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(w.temp, tb, sid, w.keys_s, w.iota, w.perm, (int) nn, 0,
@@ -1061,10 +1268,9 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     tb = w.temp_bytes;
     ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
     ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
-    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, sid,
-                       (const uint64_t *) nullptr, in_off, wire_len, in, out_off, out, flags_out, status_out,
-                       ctx->sessions, ctx->max_sessions, ctx->peer, w.state, w.powtab, w.acc, w.cnt, w.excl, w.v,
-                       w.last);
+    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
+                       w.fin, w.powtab, out, flags_out, status_out, sid, ctx->max_sessions, ctx->peer, w.acc, w.cnt,
+                       w.excl, w.last);
     ZCHECK(ctx, hipGetLastError());
     body.end();
     call.end();

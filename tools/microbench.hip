@@ -163,11 +163,13 @@ int main()
     const int blocks = 256 * 8, threads = 256;
     CHECK(hipMalloc(&buf, sizeof(uint32_t) * blocks * threads));
     const double lanes = (double) blocks * threads;
-    {
+    for (int wps = 1; wps <= 8; wps *= 2) { // waves per SIMD
         int it = 200;
-        float ms = timeit(k_salsa, buf, blocks, threads, it);
-        double blk = lanes * it;
-        printf("salsa20: %.3f ms, %.3f G blocks/s = %.1f GB/s keystream\n", ms, blk / ms / 1e6, blk * 64 / ms / 1e6);
+        const int b = 256 * wps; // 256-thread blocks: 4 waves = one per SIMD
+        float ms = timeit(k_salsa, buf, b, threads, it);
+        double blk = (double) b * threads * it;
+        printf("salsa20 @%d waves/SIMD: %.3f ms, %.3f G blocks/s = %.1f GB/s keystream\n", wps, ms, blk / ms / 1e6,
+               blk * 64 / ms / 1e6);
     }
     {
         int it = 200;

@@ -14,7 +14,8 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         short = next((k for k in keys if k in name), None)
         if not short:
             continue
-        tag = short + ("<dec>" if "ILb1E" in name else "<enc>" if "ILb0E" in name else "")
+        tag = short + ("<dec>" if ("ILb1E" in name or "<true>" in name) else
+                       "<enc>" if ("ILb0E" in name or "<false>" in name) else "")
         acc[tag][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in acc.items():
     print(k)
