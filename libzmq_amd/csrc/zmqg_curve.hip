@@ -37,6 +37,23 @@
 #ifndef ZMQG_ABLATE
 #define ZMQG_ABLATE 0
 #endif
+#ifndef ZMQG_STAMPS
+#define ZMQG_STAMPS 0
+#endif
+#if ZMQG_STAMPS // diagnostic build only: per-wave phase timestamps (tools/stamps.py)
+__device__ unsigned long long zmqg_stamp_buf[1 << 17];
+__device__ unsigned int zmqg_stamp_ctr;
+#define ZSTAMP(k)                                                                   \
+    do {                                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                          \
+        unsigned long long t_;                                                      \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                          \
+        st_[k] = t_;                                                                \
+    } while (0)
+#else
+#define ZSTAMP(k) do { } while (0)
+#endif
 
 using namespace zmqg;
 
@@ -688,6 +705,10 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
     const uint32_t total = chunk_end[n - 1];
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
+#if ZMQG_STAMPS
+        unsigned long long st_[8];
+#endif
+        ZSTAMP(0);
         const uint32_t g = base + lane;
         const uint32_t iw = wave_find_frame(chunk_end, n, base, g);
         uint32_t key = kIdle, g0 = 0, c = 0, L = 0;
@@ -733,6 +754,7 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
             prm[lane] = p;
         }
         wave_lds_fence();
+        ZSTAMP(1);
         // ---- 1. coalesced LDS-DMA of the input images
 #pragma unroll 1
         for (uint32_t k = 0; k < 17; ++k) {
@@ -746,6 +768,7 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_lds_fence();
+        ZSTAMP(2);
         // ---- 2. keystream, MAC, output image (in place, one window behind)
         uint64_t v[5] = {0, 0, 0, 0, 0};
         if (L > 0) {
@@ -815,6 +838,7 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
                 v[q] = h.l[q];
         }
         wave_lds_fence();
+        ZSTAMP(3);
         // ---- 3a. coalesced stores of the interior output granules
 #pragma unroll 1
         for (uint32_t k = 0; k < 17; ++k) {
@@ -826,6 +850,7 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
             if (pL && q >= qfirst && 16 * q + 16 <= dO + pL) // whole granule inside the chunk
                 *(GU4 *) (uintptr_t) ((pd - dO) + 16 * q) = *(const u32x4 *) (slots + 16 * idx);
         }
+        ZSTAMP(4);
         // ---- 3b. this lane's edge granules
         if (L > 0) {
             const uint32_t dO = (uint32_t) (dst & 15), end = dO + L;
@@ -856,6 +881,7 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
             }
         }
         wave_lds_fence();
+        ZSTAMP(5);
         // ---- Poly1305 combine and tag
         if (wave_segment_sum(key, v)) {
             const uint32_t i = key;
@@ -905,6 +931,15 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
                 }
             }
         }
+#if ZMQG_STAMPS
+        ZSTAMP(6);
+        if (lane == 0) {
+            const unsigned int slot = atomicAdd(&zmqg_stamp_ctr, 1u);
+            if (slot < (1u << 17) / 8)
+                for (int q = 0; q < 7; ++q)
+                    zmqg_stamp_buf[slot * 8 + q] = st_[q] - st_[0];
+        }
+#endif
     }
     (void) out_tag;
 }
@@ -1062,6 +1097,7 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
+        fprintf(stderr, "zmqg_ctx_create: %s\n", hipGetErrorString(e));
         zmqg_ctx_destroy(ctx);
         return -EIO;
     }
@@ -1123,6 +1159,28 @@ int zmqg_ctx_get_profile(zmqg_ctx *ctx, int kind, double *ms_total, uint64_t *la
     ctx->prof[kind].clear();
     return 0;
 }
+
+#if ZMQG_STAMPS
+// diagnostic build only: copy out (and reset) the per-wave phase stamps
+int zmqg_debug_stamps(unsigned long long *out, uint32_t max_records, uint32_t *count)
+{
+    unsigned int n = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&n, HIP_SYMBOL(zmqg_stamp_ctr), sizeof n) != hipSuccess)
+        return -EIO;
+    if (n > (1u << 17) / 8)
+        n = (1u << 17) / 8;
+    if (n > max_records)
+        n = max_records;
+    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(zmqg_stamp_buf), (size_t) n * 8 * sizeof(unsigned long long)) !=
+                 hipSuccess)
+        return -EIO;
+    unsigned int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(zmqg_stamp_ctr), &z, sizeof z) != hipSuccess)
+        return -EIO;
+    *count = n;
+    return 0;
+}
+#endif
 
 const char *zmqg_last_error(zmqg_ctx *ctx)
 {
