@@ -535,13 +535,14 @@ __device__ __forceinline__ void gw_window(GranuleWriter &gw, int t, const uint32
 }
 
 // ---------------------------------------------------------------- wave search
-// For the wave's chunk window [g0, g0+64): returns in every lane the frame
-// index of chunk g (first i with chunk_end[i] > g), by a 64-ary search for
-// the window's first frame (each lane tests one probe per round) and a
-// 6-step search over the <= 64 frames the window can touch.
-__device__ __forceinline__ uint32_t wave_find_frame(const uint32_t *__restrict__ chunk_end, uint32_t n, uint32_t g0,
-                                                    uint32_t g)
+// Frame lookup for a tile of 64 consecutive chunks [g0, g0+64): the frame of
+// chunk g is the first i with chunk_end[i] > g.  wave_find_lo locates the
+// tile's first frame from scratch; a wave walking consecutive tiles gets the
+// next tile's first frame from next_tile_lo instead.
+__device__ __forceinline__ uint32_t wave_find_lo(const uint32_t *__restrict__ chunk_end, uint32_t n, uint32_t g0)
 {
+    // first frame i with chunk_end[i] > g0 (the frame holding chunk g0):
+    // 64-ary search with one coalesced probe per level
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lo = 0, hi = n; // answer in [lo, hi]
     while (hi - lo > 64) {
@@ -559,15 +560,32 @@ __device__ __forceinline__ uint32_t wave_find_frame(const uint32_t *__restrict__
             hi = nhi;
         }
     }
-    {
-        const uint32_t probe = lo + lane;
-        const bool p = probe < hi && chunk_end[probe] > g0;
-        const unsigned long long m = __ballot(p);
-        lo = m ? lo + (uint32_t) __builtin_ctzll(m) : hi;
-    }
-    // frames lo .. lo+63 cover the window (each frame has >= 1 chunk)
-    const uint32_t mine = lo + lane;
-    const uint32_t ce = mine < n ? chunk_end[mine] : 0xffffffffu;
+    const uint32_t probe = lo + lane;
+    const bool p = probe < hi && chunk_end[probe] > g0;
+    const unsigned long long m = __ballot(p);
+    return m ? lo + (uint32_t) __builtin_ctzll(m) : hi;
+}
+
+// The 64 frames lo .. lo+63 cover the 64 chunks of a tile that starts in
+// frame lo (each frame has >= 1 chunk).  window_load fetches their chunk
+// ends (one coalesced load); window_find gives lane's frame for chunk g and
+// that frame's chunk end.
+__device__ __forceinline__ uint32_t window_load(const uint32_t *__restrict__ chunk_end, uint32_t n, uint32_t lo)
+{
+    // unconditional load (clamped index); window_find masks the lanes past
+    // n when it uses the value, so nothing waits for the load here
+    const uint32_t mine = lo + (threadIdx.x & 63);
+    return chunk_end[mine < n ? mine : n - 1];
+}
+
+struct FrameLook {
+    uint32_t i;  // frame holding the lane's chunk
+    uint32_t ce; // chunk_end[i]
+};
+
+__device__ __forceinline__ FrameLook window_find(uint32_t ce_raw, uint32_t lo, uint32_t n, uint32_t g)
+{
+    const uint32_t ce = lo + (threadIdx.x & 63) < n ? ce_raw : 0xffffffffu;
     uint32_t a = 0; // first lane index j with ce_j > g
 #pragma unroll
     for (int b = 32; b >= 1; b >>= 1) {
@@ -575,7 +593,16 @@ __device__ __forceinline__ uint32_t wave_find_frame(const uint32_t *__restrict__
         if (v <= g)
             a += b;
     }
-    return lo + a;
+    return FrameLook{lo + a, (uint32_t) __shfl(ce, (int) a)};
+}
+
+// First frame of the tile after the one described by `lk` (tile start t0):
+// the frame of the tile's last chunk, or the one after it if that frame ends
+// exactly at the next tile's start.
+__device__ __forceinline__ uint32_t next_tile_lo(const FrameLook &lk, uint32_t next_t0)
+{
+    const uint32_t i63 = __shfl(lk.i, 63), ce63 = __shfl(lk.ce, 63);
+    return ce63 > next_t0 ? i63 : i63 + 1;
 }
 
 } // namespace zmqg

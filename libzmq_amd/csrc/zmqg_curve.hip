@@ -61,7 +61,7 @@ namespace {
 
 constexpr int kMaxPow = 24;           // r^(16*2^k), k < 24: frames up to 2^32 bytes
 constexpr uint32_t kIdle = 0xffffffffu;
-constexpr int kBodyThreads = 256; // 4 waves x 18.5 KiB LDS staging: 2 workgroups per CU
+constexpr int kBodyThreads = 256; // 4 waves (one per SIMD) x 2 tile buffers of 18.5 KiB: one workgroup per CU
 constexpr int kHeadThreads = 256;
 
 struct DevSession {
@@ -131,6 +131,7 @@ struct Workspace {
 
 struct zmqg_ctx {
     int device = 0;
+    int cus = 256; // compute units of the device (one persistent body workgroup each)
     uint32_t max_sessions = 0;
     int sort_bits = 0;
     DevSession *sessions = nullptr;
@@ -452,24 +453,6 @@ __device__ __forceinline__ bool frame_combine(uint32_t g0, uint32_t nch, unsigne
     return true;
 }
 
-// Per-chunk contribution factor r^(Poly1305 blocks after chunk c)
-// = r^blast * (r^16)^(nch-2-c); 1 for the last chunk.
-__device__ __forceinline__ fe chunk_factor(uint32_t c, uint32_t nch, const FramePow &P, const uint32_t *powtab)
-{
-    if (c + 1 >= nch)
-        return fe_one();
-    fe f = load_fe(P.rb);
-    const uint32_t m = nch - 2 - c;
-#pragma unroll
-    for (int k = 0; k < kPowInline; ++k)
-        if ((m >> k) & 1)
-            fe_mul(f, load_fe(P.t[k]));
-    for (int k = kPowInline; (m >> k) != 0; ++k)
-        if ((m >> k) & 1)
-            fe_mul(f, load_fe(powtab + 5 * k));
-    return f;
-}
-
 // =====================================================================
 // decode
 // =====================================================================
@@ -627,15 +610,24 @@ __device__ __forceinline__ bool sequence_ok(uint64_t nonce, unsigned long long p
     return nonce > prev;
 }
 
-// Body kernel: one lane per chunk (up to 4 Salsa20 blocks = 256 stream
-// bytes).  Each lane streams its chunk with aligned 16-byte loads/stores
-// (StreamReader / GranuleWriter), so arbitrary frame offsets cost a few
-// register shifts, never divergence.
 // ---------------------------------------------------------------- body
-// One lane per chunk (up to 4 Salsa20 blocks = 256 stream bytes).  The
-// wave's 64 chunks are staged through LDS so that every global access is a
-// coalesced, aligned 16-byte granule stream (a chunk's granules go to
-// consecutive lanes), which keeps HBM/L2 traffic at the algorithmic bytes:
+// One lane per chunk (up to 4 Salsa20 blocks = 256 stream bytes); a tile is
+// 64 consecutive chunks, one wave's worth.  The kernel is persistent: one
+// workgroup of 4 waves per CU (one wave per SIMD), and each wave walks a
+// contiguous run of tiles as a two-stage software pipeline, so its HBM
+// traffic for tile t+1 is in flight while it computes tile t:
+//
+//   wait    s_waitcnt vmcnt(0): tile t's input is in LDS buffer t&1
+//   issue   tile t+1's frame records, tile t+2's chunk-end window
+//   compute windows 0-1 of tile t (LDS only)
+//   setup   tile t+1 (params, chunk factors) and its LDS-DMA into buffer ~t&1
+//   compute windows 2-3 of tile t
+//   store   tile t's output image (coalesced granules + per-lane edges)
+//   finish  Poly1305 segment sums, tags / status of the frames ending here
+//
+// Staging through LDS keeps every global access a coalesced, aligned
+// 16-byte granule stream (a chunk's granules go to consecutive lanes), so
+// HBM/L2 traffic stays at the algorithmic bytes:
 //   1. LDS-DMA (global_load_lds_dwordx4): input granule q of chunk s lands
 //      at slot s + 16q, slot = 272 bytes (17 granules), lane-linear.
 //   2. each lane works on its own slot: stream byte b is at slot + (src&15)
@@ -652,8 +644,9 @@ struct ChunkParam {
     uint32_t cont; // the next lane holds the next 256 bytes of the same frame
 };
 static_assert(sizeof(ChunkParam) == 24, "ChunkParam");
-constexpr int kWaveLds = 64 * kSlot + 64 * (int) sizeof(ChunkParam); // 18944 B
+constexpr int kWaveLds = 64 * kSlot + 64 * (int) sizeof(ChunkParam); // one tile buffer, 18944 B
 constexpr int kBodyWaves = kBodyThreads / 64;
+static_assert(kBodyWaves * 2 * kWaveLds <= 160 * 1024, "two tile buffers per wave must fit the CU's LDS");
 
 typedef __attribute__((address_space(3))) void LdsVoid;
 typedef __attribute__((address_space(1))) void GVoid;
@@ -688,190 +681,408 @@ __device__ __forceinline__ uint32_t byte_mask_below(int e, int k) // bytes [4k, 
     return b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
 }
 
+// The frame records a lane of the next tile loads (one batch of independent
+// dwordx4 loads, issued a full compute phase before they are used).  Kept
+// as raw granules so that nothing here becomes a private-memory copy.
+struct TileRecords {
+    u32x4 h[6]; // FrameHot
+    u32x4 p[7]; // FramePow
+    u32x4 f[4]; // FrameFin
+    unsigned long long ex; // decode: replay-scan exclusive max
+    uint32_t last, sid;    // decode: last frame of its session / its session
+};
+static_assert(sizeof(FrameHot) == 6 * 16 && sizeof(FramePow) == 7 * 16 && sizeof(FrameFin) == 4 * 16, "records");
+
+// Unconditional loads (an idle lane reads frame 0's records and ignores
+// them): a conditional load would need a register copy at the branch join,
+// and that copy waits for the load.
+template <bool DEC>
+__device__ __forceinline__ void load_records(TileRecords &R, uint32_t i, const FrameHot *__restrict__ hot,
+                                             const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
+                                             const unsigned long long *__restrict__ excl,
+                                             const uint8_t *__restrict__ last, const uint32_t *__restrict__ sid)
+{
+    const GCU4 *ph = (const GCU4 *) (hot + i), *pp = (const GCU4 *) (pw + i), *pf = (const GCU4 *) (fin + i);
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+        R.h[q] = ph[q];
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+        R.p[q] = pp[q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        R.f[q] = pf[q];
+    if (DEC) {
+        R.ex = excl[i];
+        R.last = last[i];
+        R.sid = sid[i];
+    } else {
+        R.ex = 0;
+        R.last = 0;
+        R.sid = 0;
+    }
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t rec_word(const u32x4 *g)
+{
+    return (W & 3) == 0 ? g[W >> 2].x : (W & 3) == 1 ? g[W >> 2].y : (W & 3) == 2 ? g[W >> 2].z : g[W >> 2].w;
+}
+
+// Per-lane state of one tile from its setup to its finish (plain words only).
+struct TileLane {
+    uint32_t key; // frame index, kIdle past the batch's last chunk
+    uint32_t g0;  // the frame's first chunk
+    uint32_t c;   // chunk index within the frame
+    uint32_t L;   // stream bytes of this chunk (0 = nothing to do)
+    uint32_t Ln;  // L of the next lane
+    uint32_t di;  // input stream byte 0 within its granule
+    uint32_t cont, prevcont;
+    uint64_t dst; // output stream byte 0
+    uint32_t f[5]; // r^(Poly1305 blocks after this chunk)
+    uint32_t k[8], n0, n1, r[5], nch, flags; // from FrameHot
+    int32_t status;
+    uint64_t out_base;
+    uint32_t hh[5], s[4], tag[4], wire_len; // from FrameFin
+    uint64_t peer_snap;
+    unsigned long long ex;
+    uint32_t last, sid;
+};
+
+template <bool DEC>
+__device__ __forceinline__ void tile_setup(TileLane &T, const TileRecords &R, bool valid, const FrameLook &lk,
+                                           uint32_t g, const uint32_t *__restrict__ powtab, uint8_t *buf)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    // Every loaded granule counts as used from here on: a record word that
+    // is never read would free its register while the load is in flight, and
+    // the next write to that register would wait for the load.
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+        asm volatile("" ::"v"(R.h[q]));
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+        asm volatile("" ::"v"(R.p[q]));
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        asm volatile("" ::"v"(R.f[q]));
+    asm volatile("" ::"v"(R.ex), "v"(R.last), "v"(R.sid));
+    // FrameHot words: key 0-7, r 8-12, nch 13, mlen 14, hl 15, n0 16, n1 17,
+    // status 18, flags 19, in_base 20-21, out_base 22-23
+    T.k[0] = rec_word<0>(R.h);
+    T.k[1] = rec_word<1>(R.h);
+    T.k[2] = rec_word<2>(R.h);
+    T.k[3] = rec_word<3>(R.h);
+    T.k[4] = rec_word<4>(R.h);
+    T.k[5] = rec_word<5>(R.h);
+    T.k[6] = rec_word<6>(R.h);
+    T.k[7] = rec_word<7>(R.h);
+    T.r[0] = rec_word<8>(R.h);
+    T.r[1] = rec_word<9>(R.h);
+    T.r[2] = rec_word<10>(R.h);
+    T.r[3] = rec_word<11>(R.h);
+    T.r[4] = rec_word<12>(R.h);
+    T.nch = rec_word<13>(R.h);
+    const uint32_t mlen = rec_word<14>(R.h), hl = rec_word<15>(R.h);
+    T.n0 = rec_word<16>(R.h);
+    T.n1 = rec_word<17>(R.h);
+    T.status = (int32_t) rec_word<18>(R.h);
+    T.flags = rec_word<19>(R.h);
+    const uint64_t in_base = ((uint64_t) rec_word<21>(R.h) << 32) | rec_word<20>(R.h);
+    T.out_base = ((uint64_t) rec_word<23>(R.h) << 32) | rec_word<22>(R.h);
+    // FrameFin words: hh 0-4, s 5-8, tag 9-12, wire_len 13, peer_snap 14-15
+    T.hh[0] = rec_word<0>(R.f);
+    T.hh[1] = rec_word<1>(R.f);
+    T.hh[2] = rec_word<2>(R.f);
+    T.hh[3] = rec_word<3>(R.f);
+    T.hh[4] = rec_word<4>(R.f);
+    T.s[0] = rec_word<5>(R.f);
+    T.s[1] = rec_word<6>(R.f);
+    T.s[2] = rec_word<7>(R.f);
+    T.s[3] = rec_word<8>(R.f);
+    T.tag[0] = rec_word<9>(R.f);
+    T.tag[1] = rec_word<10>(R.f);
+    T.tag[2] = rec_word<11>(R.f);
+    T.tag[3] = rec_word<12>(R.f);
+    T.wire_len = rec_word<13>(R.f);
+    T.peer_snap = ((uint64_t) rec_word<15>(R.f) << 32) | rec_word<14>(R.f);
+    T.ex = R.ex;
+    T.last = R.last;
+    T.sid = R.sid;
+
+    uint64_t src = 0;
+    T.key = kIdle;
+    T.g0 = 0;
+    T.c = 0;
+    T.L = 0;
+    T.dst = 0;
+    T.di = 0;
+    fe f = fe_one();
+    if (valid) {
+        const uint32_t i = lk.i;
+        T.key = i;
+        T.g0 = lk.ce - T.nch; // chunk_end[i - 1]
+        T.c = g - T.g0;
+        const uint32_t P0 = 32 + 256 * T.c; // first plaintext byte of this chunk
+        uint32_t L = mlen > P0 ? (mlen - P0 < 256 ? mlen - P0 : 256) : 0;
+        if (DEC) {
+            const uint64_t nc = ((uint64_t) bswap32(T.n0) << 32) | bswap32(T.n1);
+            if (T.status != 0 || !sequence_ok(nc, T.peer_snap, T.ex))
+                L = 0;
+            src = in_base + 32 + P0;     // ciphertext byte P0 on the wire
+            T.dst = T.out_base + P0 - 1; // plaintext byte P0 = payload byte P0-1
+        } else {
+            src = in_base + (P0 - hl);    // payload byte = plaintext byte - hl
+            T.dst = T.out_base + 32 + P0; // wire ciphertext
+        }
+        T.L = L;
+        T.di = (uint32_t) (src & 15);
+        if (L > 0 && T.c + 1 < T.nch) {
+            // chunk_factor from the raw FramePow record: r^blast * (r^16)^(nch-2-c)
+            // (words: rb 0-4, t[k] 5+5k .. 9+5k)
+            f.l[0] = rec_word<0>(R.p);
+            f.l[1] = rec_word<1>(R.p);
+            f.l[2] = rec_word<2>(R.p);
+            f.l[3] = rec_word<3>(R.p);
+            f.l[4] = rec_word<4>(R.p);
+            const uint32_t m = T.nch - 2 - T.c;
+            fe t;
+            if (m & 1) {
+                t.l[0] = rec_word<5>(R.p); t.l[1] = rec_word<6>(R.p); t.l[2] = rec_word<7>(R.p);
+                t.l[3] = rec_word<8>(R.p); t.l[4] = rec_word<9>(R.p);
+                fe_mul(f, t);
+            }
+            if (m & 2) {
+                t.l[0] = rec_word<10>(R.p); t.l[1] = rec_word<11>(R.p); t.l[2] = rec_word<12>(R.p);
+                t.l[3] = rec_word<13>(R.p); t.l[4] = rec_word<14>(R.p);
+                fe_mul(f, t);
+            }
+            if (m & 4) {
+                t.l[0] = rec_word<15>(R.p); t.l[1] = rec_word<16>(R.p); t.l[2] = rec_word<17>(R.p);
+                t.l[3] = rec_word<18>(R.p); t.l[4] = rec_word<19>(R.p);
+                fe_mul(f, t);
+            }
+            if (m & 8) {
+                t.l[0] = rec_word<20>(R.p); t.l[1] = rec_word<21>(R.p); t.l[2] = rec_word<22>(R.p);
+                t.l[3] = rec_word<23>(R.p); t.l[4] = rec_word<24>(R.p);
+                fe_mul(f, t);
+            }
+            static_assert(kPowInline == 4, "inline powers");
+            const uint32_t *pt = powtab + (size_t) i * kMaxPow * 5;
+            for (int k = kPowInline; (m >> k) != 0; ++k)
+                if ((m >> k) & 1)
+                    fe_mul(f, load_fe(pt + 5 * k));
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        T.f[q] = f.l[q];
+    const uint32_t kn = __shfl_down(T.key, 1);
+    T.Ln = __shfl_down(T.L, 1);
+    T.cont = (lane < 63 && T.key != kIdle && kn == T.key && T.L == 256 && T.Ln > 0) ? 1u : 0u;
+    T.prevcont = (__shfl_up(T.cont, 1) != 0 && lane > 0) ? 1u : 0u;
+    ChunkParam p;
+    p.src = src;
+    p.dst = T.dst;
+    p.L = T.L;
+    p.cont = T.cont;
+    ((ChunkParam *) (buf + 64 * kSlot))[lane] = p;
+}
+
+// Coalesced LDS-DMA of a tile's input images into `buf` (no wait).
+__device__ __forceinline__ void tile_dma(uint8_t *buf)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const ChunkParam *prm = (const ChunkParam *) (buf + 64 * kSlot);
+    wave_lds_fence();
+#pragma unroll 1
+    for (uint32_t k = 0; k < 17; ++k) {
+        const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
+        const uint64_t ps = prm[s].src;
+        const uint32_t pL = prm[s].L;
+        const uint32_t off = (uint32_t) (ps & 15);
+        if (pL && q < ((off + pL + 15) >> 4))
+            __builtin_amdgcn_global_load_lds((GVoid *) (uintptr_t) ((ps - off) + 16 * q),
+                                             (LdsVoid *) (buf + 1024 * k), 16, 0, 0);
+    }
+}
+
 template <bool DEC>
 __global__ __launch_bounds__(kBodyThreads) void k_body(
     uint32_t n, const uint32_t *__restrict__ chunk_end, const FrameHot *__restrict__ hot,
     const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin, const uint32_t *__restrict__ powtab,
-    uint8_t *__restrict__ out_tag, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
-    const uint32_t *__restrict__ sid, uint32_t max_sessions, unsigned long long *__restrict__ peer,
-    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
-    const uint8_t *__restrict__ last)
+    uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out, const uint32_t *__restrict__ sid,
+    uint32_t max_sessions, unsigned long long *__restrict__ peer, unsigned long long *__restrict__ acc,
+    uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl, const uint8_t *__restrict__ last)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * kWaveLds];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kWaveLds];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint8_t *slots = lds + wv * kWaveLds;
-    ChunkParam *prm = (ChunkParam *) (slots + 64 * kSlot);
-    uint8_t *myslot = slots + lane * kSlot;
+    uint8_t *const wlds = lds + wv * 2 * kWaveLds;
     const uint32_t total = chunk_end[n - 1];
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
+    const uint64_t tiles = (total + 63) >> 6;
+    const uint64_t W = (uint64_t) blockIdx.x * kBodyWaves + wv, NW = (uint64_t) gridDim.x * kBodyWaves;
+    const uint32_t tb = (uint32_t) (tiles * W / NW), te = (uint32_t) (tiles * (W + 1) / NW);
+    if (tb >= te)
+        return;
+
+    // prologue: locate tile tb from scratch, set it up and start its DMA;
+    // locate tile tb+1
+    TileLane cur;
+    FrameLook lkn = {kIdle, 0};
+    {
+        const uint32_t lo = wave_find_lo(chunk_end, n, 64 * tb);
+        const uint32_t g = 64 * tb + lane;
+        const FrameLook lk = window_find(window_load(chunk_end, n, lo), lo, n, g);
+        TileRecords R;
+        load_records<DEC>(R, g < total ? lk.i : 0, hot, pw, fin, excl, last, sid);
+        tile_setup<DEC>(cur, R, g < total, lk, g, powtab, wlds);
+        tile_dma(wlds);
+        if (tb + 1 < te) {
+            const uint32_t lo1 = next_tile_lo(lk, 64 * (tb + 1));
+            lkn = window_find(window_load(chunk_end, n, lo1), lo1, n, 64 * (tb + 1) + lane);
+        }
+    }
+
+#pragma unroll 1
+    for (uint32_t t = tb; t < te; ++t) {
 #if ZMQG_STAMPS
         unsigned long long st_[8];
 #endif
         ZSTAMP(0);
-        const uint32_t g = base + lane;
-        const uint32_t iw = wave_find_frame(chunk_end, n, base, g);
-        uint32_t key = kIdle, g0 = 0, c = 0, L = 0;
-        uint64_t src = 0, dst = 0;
-        FrameHot H;
-        fe f = fe_one();
-        if (g < total) {
-            const uint32_t i = iw;
-            key = i;
-            g0 = i ? chunk_end[i - 1] : 0;
-            c = g - g0;
-            H = hot[i];
-            const FramePow Pw = pw[i];
-            unsigned long long ex = 0, psnap = 0;
-            if (DEC) {
-                ex = excl[i];
-                psnap = fin[i].peer_snap;
-            }
-            const uint32_t P0 = 32 + 256 * c; // first plaintext byte of this chunk
-            L = H.mlen > P0 ? (H.mlen - P0 < 256 ? H.mlen - P0 : 256) : 0;
-            if (DEC) {
-                const uint64_t nc = ((uint64_t) bswap32(H.n0) << 32) | bswap32(H.n1);
-                if (H.status != 0 || !sequence_ok(nc, psnap, ex))
-                    L = 0;
-                src = H.in_base + 32 + P0;  // ciphertext byte P0 on the wire
-                dst = H.out_base + P0 - 1;  // plaintext byte P0 = payload byte P0-1
-            } else {
-                src = H.in_base + (P0 - H.hl); // payload byte = plaintext byte - hl
-                dst = H.out_base + 32 + P0;    // wire ciphertext
-            }
-            if (L > 0)
-                f = chunk_factor(c, H.nch, Pw, powtab + (size_t) i * kMaxPow * 5);
-        }
-        const uint32_t kn = __shfl_down(key, 1), Ln = __shfl_down(L, 1);
-        const bool cont = lane < 63 && key != kIdle && kn == key && L == 256 && Ln > 0;
-        const bool prevcont = __shfl_up(cont ? 1u : 0u, 1) != 0 && lane > 0;
-        {
-            ChunkParam p;
-            p.src = src;
-            p.dst = dst;
-            p.L = L;
-            p.cont = cont ? 1u : 0u;
-            prm[lane] = p;
-        }
+        uint8_t *const cb = wlds + ((t - tb) & 1) * kWaveLds;
+        uint8_t *const nb = wlds + (((t - tb) & 1) ^ 1) * kWaveLds;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile t's DMA (and everything before it)
         wave_lds_fence();
         ZSTAMP(1);
-        // ---- 1. coalesced LDS-DMA of the input images
-#pragma unroll 1
-        for (uint32_t k = 0; k < 17; ++k) {
-            const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
-            const uint64_t ps = prm[s].src;
-            const uint32_t pL = prm[s].L;
-            const uint32_t off = (uint32_t) (ps & 15);
-            if (pL && q < ((off + pL + 15) >> 4))
-                __builtin_amdgcn_global_load_lds((GVoid *) (uintptr_t) ((ps - off) + 16 * q),
-                                                 (LdsVoid *) (slots + 1024 * k), 16, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wave_lds_fence();
-        ZSTAMP(2);
-        // ---- 2. keystream, MAC, output image (in place, one window behind)
+        const bool has_next = t + 1 < te, has_next2 = t + 2 < te;
+        // ---- issue: next tile's records, the chunk-end window after it
+        const uint32_t gn = 64 * (t + 1) + lane;
+        TileRecords Rn;
+        load_records<DEC>(Rn, has_next && gn < total ? lkn.i : 0, hot, pw, fin, excl, last, sid);
+        // (unconditional: on the last two tiles this reads a clamped, unused window)
+        const uint32_t lo2 = next_tile_lo(lkn, 64 * (t + 2));
+        const uint32_t ce2 = window_load(chunk_end, n, lo2 < n ? lo2 : n - 1);
+        // ---- compute: keystream, MAC, output image (in place, one window behind)
         uint64_t v[5] = {0, 0, 0, 0, 0};
-        if (L > 0) {
-            const fe r = load_fe(H.r);
-            const uint32_t di = (uint32_t) (src & 15), dO = (uint32_t) (dst & 15);
-            const uint32_t *inw = (const uint32_t *) (myslot + (di & ~3u));
-            uint32_t *outw = (uint32_t *) (myslot + (dO & ~3u));
-            const uint32_t si = di & 3, so = dO & 3;
-            const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
-            const uint32_t nwin = (L + 63) >> 6;
-            fe h = fe_zero();
-            uint32_t d[17];
+        const uint32_t L = cur.L, nwin = (L + 63) >> 6;
+        const uint32_t dO = (uint32_t) (cur.dst & 15), si = cur.di & 3, so = dO & 3;
+        uint8_t *const myslot = cb + lane * kSlot;
+        const uint32_t *inw = (const uint32_t *) (myslot + (cur.di & ~3u));
+        uint32_t *outw = (uint32_t *) (myslot + (dO & ~3u));
+        const fe r = load_fe(cur.r);
+        const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+        fe h = fe_zero();
+        uint32_t d[17];
+        uint32_t carry = 0;
+        if (nwin) {
 #pragma unroll
             for (int q = 0; q < 17; ++q)
                 d[q] = inw[q];
-            uint32_t carry = 0;
-            for (uint32_t t = 0; t < nwin; ++t) {
-                const int nv = L - 64 * t >= 64 ? 64 : (int) (L - 64 * t);
-                uint32_t w[16], ks[16];
+        }
+        auto window = [&](uint32_t tw) {
+            const int nv = L - 64 * tw >= 64 ? 64 : (int) (L - 64 * tw);
+            uint32_t w[16], ks[16];
 #pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    w[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], si);
-                if (t + 1 < nwin) { // read ahead before this window's output overwrites it
+            for (int q = 0; q < 16; ++q)
+                w[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], si);
+            if (tw + 1 < nwin) { // read ahead before this window's output overwrites it
 #pragma unroll
-                    for (int q = 0; q < 17; ++q)
-                        d[q] = inw[16 * (t + 1) + q];
-                }
-                if (nv < 64)
-                    mask_tail(w, nv);
+                for (int q = 0; q < 17; ++q)
+                    d[q] = inw[16 * (tw + 1) + q];
+            }
+            if (nv < 64)
+                mask_tail(w, nv);
 #if ZMQG_ABLATE == 2 // timing experiment only: memory traffic without keystream/MAC work
 #pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    ks[q] = t * 16 + q;
+            for (int q = 0; q < 16; ++q)
+                ks[q] = tw * 16 + q;
 #else
-                salsa20_block(ks, H.key, H.n0, H.n1, 1 + 4 * c + t, 0);
+            salsa20_block(ks, cur.k, cur.n0, cur.n1, 1 + 4 * cur.c + tw, 0);
 #endif
-                if (DEC && ZMQG_ABLATE != 2)
-                    poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+            if (DEC && ZMQG_ABLATE != 2)
+                poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                w[q] ^= ks[q];
+            if (nv < 64)
+                mask_tail(w, nv);
+            if (!DEC && ZMQG_ABLATE != 2)
+                poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+#if ZMQG_ABLATE == 2
+            h.l[0] ^= w[0];
+#endif
+            // image dword (dO>>2) + 16tw + q holds stream bytes [64tw + 4q - so, +4)
+            if (so == 0) {
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
-                    w[q] ^= ks[q];
-                if (nv < 64)
-                    mask_tail(w, nv);
-                if (!DEC && ZMQG_ABLATE != 2)
-                    poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
-#if ZMQG_ABLATE == 2
-                h.l[0] ^= w[0];
-#endif
-                // image dword (dO>>2) + 16t + q holds stream bytes [64t + 4q - so, +4)
-                if (so == 0) {
+                    outw[16 * tw + q] = w[q];
+            } else {
+                outw[16 * tw] = __builtin_amdgcn_alignbyte(w[0], carry, 4 - so);
 #pragma unroll
-                    for (int q = 0; q < 16; ++q)
-                        outw[16 * t + q] = w[q];
-                } else {
-                    outw[16 * t] = __builtin_amdgcn_alignbyte(w[0], carry, 4 - so);
-#pragma unroll
-                    for (int q = 1; q < 16; ++q)
-                        outw[16 * t + q] = __builtin_amdgcn_alignbyte(w[q], w[q - 1], 4 - so);
-                    carry = w[15];
-                    if (t + 1 == nwin)
-                        outw[16 * t + 16] = __builtin_amdgcn_alignbyte(0u, w[15], 4 - so);
-                }
+                for (int q = 1; q < 16; ++q)
+                    outw[16 * tw + q] = __builtin_amdgcn_alignbyte(w[q], w[q - 1], 4 - so);
+                carry = w[15];
+                if (tw + 1 == nwin)
+                    outw[16 * tw + 16] = __builtin_amdgcn_alignbyte(0u, w[15], 4 - so);
             }
-            fe_mul(h, f);
+        };
+        const uint32_t nw1 = nwin < 2 ? nwin : 2;
+        for (uint32_t tw = 0; tw < nw1; ++tw)
+            window(tw);
+        ZSTAMP(2);
+        // ---- setup: next tile's params and its DMA; locate the tile after it
+        // (on the wave's last tile this sets up an all-idle tile: no DMA)
+        TileLane nx;
+        tile_setup<DEC>(nx, Rn, has_next && gn < total, lkn, gn, powtab, nb);
+        tile_dma(nb);
+        FrameLook lk2 = {kIdle, 0};
+        if (has_next2)
+            lk2 = window_find(ce2, lo2, n, 64 * (t + 2) + lane);
+        ZSTAMP(3);
+        for (uint32_t tw = 2; tw < nwin; ++tw)
+            window(tw);
+        if (L > 0) {
+            fe_mul(h, load_fe(cur.f));
 #pragma unroll
             for (int q = 0; q < 5; ++q)
                 v[q] = h.l[q];
         }
         wave_lds_fence();
-        ZSTAMP(3);
-        // ---- 3a. coalesced stores of the interior output granules
-#pragma unroll 1
-        for (uint32_t k = 0; k < 17; ++k) {
-            const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
-            const uint64_t pd = prm[s].dst;
-            const uint32_t pL = prm[s].L;
-            const uint32_t dO = (uint32_t) (pd & 15);
-            const uint32_t qfirst = dO ? 1u : 0u;          // granule 0 is an edge when misaligned
-            if (pL && q >= qfirst && 16 * q + 16 <= dO + pL) // whole granule inside the chunk
-                *(GU4 *) (uintptr_t) ((pd - dO) + 16 * q) = *(const u32x4 *) (slots + 16 * idx);
-        }
         ZSTAMP(4);
-        // ---- 3b. this lane's edge granules
+        // ---- store: coalesced interior granules, then this lane's edges
+        {
+            const ChunkParam *prm = (const ChunkParam *) (cb + 64 * kSlot);
+#pragma unroll 1
+            for (uint32_t k = 0; k < 17; ++k) {
+                const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
+                const uint64_t pd = prm[s].dst;
+                const uint32_t pL = prm[s].L;
+                const uint32_t pO = (uint32_t) (pd & 15);
+                const uint32_t qfirst = pO ? 1u : 0u;          // granule 0 is an edge when misaligned
+                if (pL && q >= qfirst && 16 * q + 16 <= pO + pL) // whole granule inside the chunk
+                    *(GU4 *) (uintptr_t) ((pd - pO) + 16 * q) = *(const u32x4 *) (cb + 16 * idx);
+            }
+        }
         if (L > 0) {
-            const uint32_t dO = (uint32_t) (dst & 15), end = dO + L;
-            GU8 *gbase = (GU8 *) (uintptr_t) (dst - dO);
+            const uint32_t end = dO + L;
+            GU8 *gbase = (GU8 *) (uintptr_t) (cur.dst - dO);
             const uint32_t ql = end >> 4, el = end & 15; // granule of the last byte / its valid bytes
-            if (dO && !prevcont) { // front edge [dO, min(16, end)) (merged by the previous chunk otherwise)
+            if (dO && !cur.prevcont) { // front edge [dO, min(16, end)) (merged by the previous chunk otherwise)
                 const u32x4 gv = *(const u32x4 *) myslot;
                 store_granule_range(gbase, (int) dO, end < 16 ? (int) end : 16, gv);
             }
             if (el && (ql >= 1 || dO == 0)) { // back edge [0, el) (granule 0 with dO > 0 was the front edge)
                 u32x4 gv = *(const u32x4 *) (myslot + 16 * ql);
                 int hi = (int) el;
-                if (cont) { // the next chunk's bytes [el, el + L_next) complete it
-                    const u32x4 nx = *(const u32x4 *) (myslot + kSlot);
-                    const int hn = (int) el + (int) Ln;
+                if (cur.cont) { // the next chunk's bytes [el, el + L_next) complete it
+                    const u32x4 nx4 = *(const u32x4 *) (myslot + kSlot);
+                    const int hn = (int) el + (int) cur.Ln;
                     const uint32_t m0 = byte_mask_below(hi, 0), m1 = byte_mask_below(hi, 1),
                                    m2 = byte_mask_below(hi, 2), m3 = byte_mask_below(hi, 3);
-                    gv.x = (gv.x & m0) | (nx.x & ~m0);
-                    gv.y = (gv.y & m1) | (nx.y & ~m1);
-                    gv.z = (gv.z & m2) | (nx.z & ~m2);
-                    gv.w = (gv.w & m3) | (nx.w & ~m3);
+                    gv.x = (gv.x & m0) | (nx4.x & ~m0);
+                    gv.y = (gv.y & m1) | (nx4.y & ~m1);
+                    gv.z = (gv.z & m2) | (nx4.z & ~m2);
+                    gv.w = (gv.w & m3) | (nx4.w & ~m3);
                     hi = hn < 16 ? hn : 16;
                 }
                 if (hi == 16)
@@ -880,53 +1091,50 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
                     store_granule_range(gbase + 16 * ql, 0, hi, gv);
             }
         }
-        wave_lds_fence();
         ZSTAMP(5);
-        // ---- Poly1305 combine and tag
-        if (wave_segment_sum(key, v)) {
-            const uint32_t i = key;
-            const FrameHot &H = hot[i];
-            if (frame_combine(g0, H.nch, acc + (size_t) i * 5, cnt + i, v)) {
-                const FrameFin F = fin[i];
+        // ---- finish: Poly1305 combine and tag / status
+        if (wave_segment_sum(cur.key, v)) {
+            const uint32_t i = cur.key;
+            if (frame_combine(cur.g0, cur.nch, acc + (size_t) i * 5, cnt + i, v)) {
                 if (!DEC) {
 #pragma unroll
                     for (int q = 0; q < 5; ++q)
-                        v[q] += F.hh[q];
+                        v[q] += cur.hh[q];
                     uint32_t tag[16];
-                    poly_finish(fe_from_wide(v), F.s, tag);
-                    store_window((uint8_t *) (uintptr_t) H.out_base + 16, 16, tag);
+                    poly_finish(fe_from_wide(v), cur.s, tag);
+                    store_window((uint8_t *) (uintptr_t) cur.out_base + 16, 16, tag);
                 } else {
-                    int32_t status = H.status;
-                    const unsigned long long ex = excl[i];
-                    const uint64_t nc = ((uint64_t) bswap32(H.n0) << 32) | bswap32(H.n1);
-                    if (status == 0 && !sequence_ok(nc, F.peer_snap, ex))
+                    int32_t status = cur.status;
+                    const unsigned long long ex = cur.ex;
+                    const uint64_t nc = ((uint64_t) bswap32(cur.n0) << 32) | bswap32(cur.n1);
+                    if (status == 0 && !sequence_ok(nc, cur.peer_snap, ex))
                         status = ZMQG_ERR_INVALID_SEQUENCE;
                     if (status == 0) {
 #pragma unroll
                         for (int q = 0; q < 5; ++q)
-                            v[q] += F.hh[q];
+                            v[q] += cur.hh[q];
                         uint32_t tag[4];
-                        poly_finish(fe_from_wide(v), F.s, tag);
-                        const uint32_t diff =
-                            (tag[0] ^ F.tag[0]) | (tag[1] ^ F.tag[1]) | (tag[2] ^ F.tag[2]) | (tag[3] ^ F.tag[3]);
+                        poly_finish(fe_from_wide(v), cur.s, tag);
+                        const uint32_t diff = (tag[0] ^ cur.tag[0]) | (tag[1] ^ cur.tag[1]) | (tag[2] ^ cur.tag[2]) |
+                                              (tag[3] ^ cur.tag[3]);
                         if (diff)
                             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
                     }
                     status_out[i] = status;
-                    flags_out[i] = status == 0 ? (uint8_t) H.flags : 0;
-                    if (status != 0 && F.wire_len >= 33) {
-                        uint8_t *o = (uint8_t *) (uintptr_t) H.out_base;
-                        for (uint32_t b = 0; b < F.wire_len - 33; ++b)
+                    flags_out[i] = status == 0 ? (uint8_t) cur.flags : 0;
+                    if (status != 0 && cur.wire_len >= 33) {
+                        uint8_t *o = (uint8_t *) (uintptr_t) cur.out_base;
+                        for (uint32_t b = 0; b < cur.wire_len - 33; ++b)
                             o[b] = 0;
                     }
-                    if (last[i]) {
+                    if (cur.last) {
                         // _cn_peer_nonce after the batch: max over accepted headers
-                        unsigned long long p = F.peer_snap;
+                        unsigned long long p = cur.peer_snap;
                         if (ex > p)
                             p = ex;
-                        if (H.status == 0 && nc > p)
+                        if (cur.status == 0 && nc > p)
                             p = nc;
-                        peer[sid[i] < max_sessions ? sid[i] : 0] = p;
+                        peer[cur.sid < max_sessions ? cur.sid : 0] = p;
                     }
                 }
             }
@@ -940,8 +1148,9 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
                     zmqg_stamp_buf[slot * 8 + q] = st_[q] - st_[0];
         }
 #endif
+        cur = nx;
+        lkn = lk2;
     }
-    (void) out_tag;
 }
 
 } // namespace
@@ -1009,12 +1218,10 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
     return 0;
 }
 
-uint32_t body_grid(uint64_t n)
+uint32_t body_grid(const zmqg_ctx *ctx)
 {
-    // one lane per 256-byte chunk; 4 workgroups of 4 waves per CU on the
-    // 256 CUs of an MI355X (4 waves per SIMD), grid-stride beyond.
-    (void) n;
-    return 1024;
+    // persistent: one workgroup (4 waves, one per SIMD) per compute unit
+    return ctx->cus > 0 ? (uint32_t) ctx->cus : 256u;
 }
 
 int check_n(uint64_t n)
@@ -1094,6 +1301,8 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
         e = hipMalloc((void **) &ctx->peer, sizeof(unsigned long long) * max_sessions);
     if (e == hipSuccess)
         e = hipMemset(ctx->peer, 0, sizeof(unsigned long long) * max_sessions);
+    if (e == hipSuccess)
+        e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1275,8 +1484,8 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     size_t tb = w.temp_bytes;
     ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
     ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
-    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
-                       w.fin, w.powtab, out, (uint8_t *) nullptr, (int32_t *) nullptr, sid, ctx->max_sessions,
+    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
+                       w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, sid, ctx->max_sessions,
                        ctx->peer, w.acc, w.cnt, (const unsigned long long *) nullptr, (const uint8_t *) nullptr);
     ZCHECK(ctx, hipGetLastError());
     body.end();
@@ -1326,8 +1535,8 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     tb = w.temp_bytes;
     ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
     ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
-    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(n)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
-                       w.fin, w.powtab, out, flags_out, status_out, sid, ctx->max_sessions, ctx->peer, w.acc, w.cnt,
+    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
+                       w.fin, w.powtab, flags_out, status_out, sid, ctx->max_sessions, ctx->peer, w.acc, w.cnt,
                        w.excl, w.last);
     ZCHECK(ctx, hipGetLastError());
     body.end();

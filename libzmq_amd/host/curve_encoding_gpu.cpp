@@ -1,0 +1,181 @@
+// curve_encoding_gpu.cpp -- see curve_encoding_gpu.hpp.
+#include "curve_encoding_gpu.hpp"
+
+#include <errno.h>
+#include <string.h>
+
+namespace zmqg
+{
+curve_encoding_gpu_t::curve_encoding_gpu_t (zmqg_ctx *ctx_,
+                                            uint32_t sid_,
+                                            const char *encode_nonce_prefix_,
+                                            const char *decode_nonce_prefix_,
+                                            bool downgrade_sub_) :
+    _ctx (ctx_),
+    _sid (sid_),
+    _cn_nonce (1), // src/curve_mechanism_base.cpp:20-21
+    _installed (false),
+    _downgrade_sub (downgrade_sub_)
+{
+    memcpy (_encode_nonce_prefix, encode_nonce_prefix_, 16);
+    memcpy (_decode_nonce_prefix, decode_nonce_prefix_, 16);
+    memset (_cn_precom, 0, sizeof _cn_precom);
+    memset (_installed_precom, 0, sizeof _installed_precom);
+}
+
+int curve_encoding_gpu_t::sync_session ()
+{
+    if (_installed
+        && memcmp (_installed_precom, _cn_precom, sizeof _cn_precom) == 0)
+        return 0;
+    //  the reference's _cn_peer_nonce starts at 1 (curve_mechanism_base.cpp:21)
+    uint64_t peer = 1;
+    if (_installed && zmqg_session_get_peer_nonce (_ctx, _sid, &peer) != 0)
+        return -1;
+    if (zmqg_session_set (_ctx, _sid, _cn_precom, _encode_nonce_prefix,
+                          _decode_nonce_prefix, _downgrade_sub ? 1 : 0, peer)
+        != 0)
+        return -1;
+    memcpy (_installed_precom, _cn_precom, sizeof _cn_precom);
+    _installed = true;
+    return 0;
+}
+
+void curve_encoding_gpu_t::set_peer_nonce (nonce_t peer_nonce_)
+{
+    if (sync_session () == 0)
+        zmqg_session_set_peer_nonce (_ctx, _sid, peer_nonce_);
+}
+
+curve_encoding_gpu_t::nonce_t curve_encoding_gpu_t::get_peer_nonce () const
+{
+    uint64_t p = 0;
+    zmqg_session_get_peer_nonce (_ctx, _sid, &p);
+    return p;
+}
+
+int curve_encoding_gpu_t::encode (msg_buf_t *msg_)
+{
+    curve_encoding_gpu_t *e = this;
+    return encode_many (&e, &msg_, 1);
+}
+
+int curve_encoding_gpu_t::decode (msg_buf_t *msg_, int *error_event_code_)
+{
+    curve_encoding_gpu_t *d = this;
+    int32_t status = 0;
+    if (decode_many (&d, &msg_, 1, &status) != 0)
+        return -1;
+    if (status != 0) {
+        //  src/curve_mechanism_base.cpp:84-108, 277-281
+        if (error_event_code_)
+            *error_event_code_ = status;
+        errno = EPROTO;
+        return -1;
+    }
+    return 0;
+}
+
+int curve_encoding_gpu_t::encode_many (curve_encoding_gpu_t *const *enc_,
+                                       msg_buf_t *const *msgs_,
+                                       size_t n_)
+{
+    if (n_ == 0)
+        return 0;
+    zmqg_ctx *ctx = enc_[0]->_ctx;
+    std::vector<uint32_t> sid (n_), len (n_);
+    std::vector<uint64_t> nonce (n_), in_off (n_), out_off (n_);
+    std::vector<uint8_t> flags (n_);
+    uint64_t in_bytes = 0, out_bytes = 0;
+    for (size_t i = 0; i < n_; ++i) {
+        curve_encoding_gpu_t *e = enc_[i];
+        if (e->_ctx != ctx || msgs_[i]->size () > 0xffffffffu) {
+            errno = EINVAL;
+            return -1;
+        }
+        if (e->sync_session () != 0) {
+            errno = EIO;
+            return -1;
+        }
+        sid[i] = e->_sid;
+        nonce[i] = e->get_and_inc_nonce (); // src/curve_mechanism_base.cpp:114-116
+        flags[i] = msgs_[i]->flags;
+        len[i] = (uint32_t) msgs_[i]->size ();
+        in_off[i] = in_bytes;
+        in_bytes += len[i];
+        out_off[i] = out_bytes;
+        out_bytes +=
+          zmqg_wire_size (flags[i], e->_downgrade_sub ? 1 : 0, len[i]);
+    }
+    std::vector<uint8_t> in (in_bytes ? in_bytes : 1), out (out_bytes);
+    for (size_t i = 0; i < n_; ++i)
+        if (len[i])
+            memcpy (&in[in_off[i]], msgs_[i]->data (), len[i]);
+    const int rc =
+      zmqg_encode_host (ctx, n_, &sid[0], &nonce[0], &flags[0], &in_off[0],
+                        &len[0], &in[0], in_bytes, &out_off[0], &out[0],
+                        out_bytes);
+    if (rc != 0) {
+        errno = -rc;
+        return -1;
+    }
+    for (size_t i = 0; i < n_; ++i) {
+        const uint64_t end = i + 1 < n_ ? out_off[i + 1] : out_bytes;
+        msgs_[i]->bytes.assign (out.begin () + out_off[i], out.begin () + end);
+        msgs_[i]->flags = 0; // the boxed message is a fresh msg_t
+    }
+    return 0;
+}
+
+int curve_encoding_gpu_t::decode_many (curve_encoding_gpu_t *const *dec_,
+                                       msg_buf_t *const *msgs_,
+                                       size_t n_,
+                                       int32_t *status_out_)
+{
+    if (n_ == 0)
+        return 0;
+    zmqg_ctx *ctx = dec_[0]->_ctx;
+    std::vector<uint32_t> sid (n_), wire_len (n_);
+    std::vector<uint64_t> in_off (n_), out_off (n_);
+    uint64_t in_bytes = 0, out_bytes = 0;
+    for (size_t i = 0; i < n_; ++i) {
+        curve_encoding_gpu_t *d = dec_[i];
+        if (d->_ctx != ctx || msgs_[i]->size () > 0xffffffffu) {
+            errno = EINVAL;
+            return -1;
+        }
+        if (d->sync_session () != 0) {
+            errno = EIO;
+            return -1;
+        }
+        sid[i] = d->_sid;
+        wire_len[i] = (uint32_t) msgs_[i]->size ();
+        in_off[i] = in_bytes;
+        in_bytes += wire_len[i];
+        out_off[i] = out_bytes;
+        out_bytes += wire_len[i] >= 33 ? wire_len[i] - 33 : 0;
+    }
+    std::vector<uint8_t> in (in_bytes ? in_bytes : 1),
+      out (out_bytes ? out_bytes : 1), flags (n_);
+    for (size_t i = 0; i < n_; ++i)
+        if (wire_len[i])
+            memcpy (&in[in_off[i]], msgs_[i]->data (), wire_len[i]);
+    const int rc = zmqg_decode_host (ctx, n_, &sid[0], &in_off[0],
+                                     &wire_len[0], &in[0], in_bytes,
+                                     &out_off[0], &out[0], out_bytes,
+                                     &flags[0], status_out_);
+    if (rc != 0) {
+        errno = -rc;
+        return -1;
+    }
+    for (size_t i = 0; i < n_; ++i) {
+        if (status_out_[i] != 0)
+            continue; // the reference leaves a failed message undecrypted
+        const uint64_t plen = wire_len[i] - 33;
+        msgs_[i]->bytes.assign (out.begin () + out_off[i],
+                                out.begin () + out_off[i] + plen);
+        msgs_[i]->flags |= flags[i]; // msg_t::set_flags ORs (src/msg.cpp:433-436)
+    }
+    return 0;
+}
+}
