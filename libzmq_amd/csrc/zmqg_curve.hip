@@ -14,8 +14,8 @@
 //   replay scan   decode only: per-session exclusive prefix max of accepted
 //                 nonces in batch order (hipCUB), = the reference's
 //                 sequential _cn_peer_nonce rule.
-//   body kernel   one lane per chunk = 4 Salsa20 blocks = 256 ciphertext
-//                 bytes = 16 Poly1305 blocks; lanes of a frame are adjacent,
+//   body kernel   one lane per chunk = 2 Salsa20 blocks = 128 ciphertext
+//                 bytes = 8 Poly1305 blocks; lanes of a frame are adjacent,
 //                 so the per-chunk Poly1305 partials (each multiplied by its
 //                 power of r) are summed by a segmented wave reduction and
 //                 the segment leader finishes the tag; frames spanning
@@ -59,9 +59,10 @@ using namespace zmqg;
 
 namespace {
 
-constexpr int kMaxPow = 24;           // r^(16*2^k), k < 24: frames up to 2^32 bytes
+constexpr uint32_t kChunk = 128;      // body chunk: 2 Salsa20 blocks = 8 Poly1305 blocks per lane
+constexpr int kMaxPow = 25;           // r^(8*2^k), k < 25: frames up to 2^32 bytes
 constexpr uint32_t kIdle = 0xffffffffu;
-constexpr int kBodyThreads = 256; // 4 waves (one per SIMD) x 2 tile buffers of 18.5 KiB: one workgroup per CU
+constexpr int kBodyThreads = 256; // 4 waves x 2 tile buffers of 9 KiB: 2 workgroups (8 waves) per CU
 constexpr int kHeadThreads = 256;
 
 struct DevSession {
@@ -88,10 +89,10 @@ struct __attribute__((aligned(16))) FrameHot { // needed to start a chunk (96 B)
 };
 static_assert(sizeof(FrameHot) == 96, "FrameHot layout");
 
-constexpr int kPowInline = 4; // r^(16*2^k) for k < 4 kept in the record (frames up to 17 chunks)
+constexpr int kPowInline = 4; // r^(8*2^k) for k < 4 kept in the record (frames up to 17 chunks)
 struct __attribute__((aligned(16))) FramePow { // chunk factor inputs (112 B)
     uint32_t rb[5];                // r^(Poly1305 blocks in the last chunk)
-    uint32_t t[kPowInline][5];     // r^(16*2^k)
+    uint32_t t[kPowInline][5];     // r^(8*2^k)
     uint32_t pad[3];
 };
 static_assert(sizeof(FramePow) == 112, "FramePow layout");
@@ -192,14 +193,15 @@ __device__ __forceinline__ void body_geometry(uint32_t mlen, uint32_t &nch, uint
         return;
     }
     const uint32_t body = mlen - 32;
-    nch = (body + 255) / 256;
-    const uint32_t lastb = body - 256 * (nch - 1);
+    nch = (body + kChunk - 1) / kChunk;
+    const uint32_t lastb = body - kChunk * (nch - 1);
     blast = (lastb + 15) / 16;
 }
 
-// Computes r^blast and r^(16*2^k) for k < bits(nch-1) (the first kPowInline
+// Computes r^blast and r^(8*2^k) for k < bits(nch-1) (the first kPowInline
 // into the frame record, the rest into powtab), and returns the head factor
-// r^(body blocks) = r^blast * (r^16)^(nch-1).
+// r^(body blocks) = r^blast * (r^8)^(nch-1).
+static_assert(kChunk == 128, "head_powers assumes 8 Poly1305 blocks per chunk");
 __device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, FramePow *P, uint32_t *powtab, fe &head_factor)
 {
     fe r2 = r;
@@ -208,11 +210,9 @@ __device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, FramePow 
     fe_mul(r4, r2);
     fe r8 = r4;
     fe_mul(r8, r4);
-    fe r16 = r8;
-    fe_mul(r16, r8);
     fe rb = fe_one();
-    if (blast == 16) {
-        rb = r16;
+    if (blast == 8) {
+        rb = r8;
     } else {
         if (blast & 1)
             fe_mul(rb, r);
@@ -220,16 +220,14 @@ __device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, FramePow 
             fe_mul(rb, r2);
         if (blast & 4)
             fe_mul(rb, r4);
-        if (blast & 8)
-            fe_mul(rb, r8);
     }
     store_fe(P->rb, rb);
 #pragma unroll
     for (int k = 0; k < kPowInline; ++k)
         store_fe(P->t[k], fe_zero());
     head_factor = rb;
-    const uint32_t m = nch - 1; // head multiplies by (r^16)^(nch-1)
-    fe t = r16;
+    const uint32_t m = nch - 1; // head multiplies by (r^8)^(nch-1)
+    fe t = r8;
     for (int k = 0; (m >> k) != 0; ++k) {
         if (k < kPowInline)
             store_fe(P->t[k], t); // global record: a runtime index is fine here
@@ -611,42 +609,40 @@ __device__ __forceinline__ bool sequence_ok(uint64_t nonce, unsigned long long p
 }
 
 // ---------------------------------------------------------------- body
-// One lane per chunk (up to 4 Salsa20 blocks = 256 stream bytes); a tile is
-// 64 consecutive chunks, one wave's worth.  The kernel is persistent: one
-// workgroup of 4 waves per CU (one wave per SIMD), and each wave walks a
-// contiguous run of tiles as a two-stage software pipeline, so its HBM
-// traffic for tile t+1 is in flight while it computes tile t:
+// One lane per chunk (2 Salsa20 blocks = 128 stream bytes = 8 Poly1305
+// blocks); a tile is 64 consecutive chunks, one wave's worth, so a tile's
+// input and output are each one (nearly) contiguous 8 KiB stream.  The
+// kernel is persistent with two waves per SIMD (two workgroups of 4 waves
+// per CU), and each wave walks a contiguous run of tiles as a two-stage
+// software pipeline, so its HBM traffic for tile t+1 is in flight while it
+// computes tile t (and the other wave on the SIMD covers the rest):
 //
 //   wait    s_waitcnt vmcnt(0): tile t's input is in LDS buffer t&1
 //   issue   tile t+1's frame records, tile t+2's chunk-end window
-//   compute windows 0-1 of tile t (LDS only)
+//   compute window 0 of tile t (LDS only)
 //   setup   tile t+1 (params, chunk factors) and its LDS-DMA into buffer ~t&1
-//   compute windows 2-3 of tile t
+//   compute window 1 of tile t
 //   store   tile t's output image (coalesced granules + per-lane edges)
 //   finish  Poly1305 segment sums, tags / status of the frames ending here
 //
 // Staging through LDS keeps every global access a coalesced, aligned
-// 16-byte granule stream (a chunk's granules go to consecutive lanes), so
-// HBM/L2 traffic stays at the algorithmic bytes:
+// 16-byte granule stream (a chunk's granules go to consecutive lanes):
 //   1. LDS-DMA (global_load_lds_dwordx4): input granule q of chunk s lands
-//      at slot s + 16q, slot = 272 bytes (17 granules), lane-linear.
+//      at slot s + 16q, slot = 144 bytes (9 granules), lane-linear.
 //   2. each lane works on its own slot: stream byte b is at slot + (src&15)
 //      + b; the output image (stream byte b at slot + (dst&15) + b) is
 //      written in place, one window behind the input it has already read.
 //   3. interior output granules go back with coalesced dwordx4 stores;
 //      each lane then stores its own (at most two) edge granules, merging
 //      the granule it shares with the next chunk of the same frame.
-constexpr int kSlot = 272;
-struct ChunkParam {
-    uint64_t src; // input stream byte 0 (global address)
-    uint64_t dst; // output stream byte 0 (global address)
-    uint32_t L;   // stream bytes of this chunk (0 = none)
-    uint32_t cont; // the next lane holds the next 256 bytes of the same frame
-};
-static_assert(sizeof(ChunkParam) == 24, "ChunkParam");
-constexpr int kWaveLds = 64 * kSlot + 64 * (int) sizeof(ChunkParam); // one tile buffer, 18944 B
+// Chunk parameters for the cooperative DMA/store rounds come from the
+// owning lane by ds_bpermute, so LDS holds nothing but the two tile images.
+constexpr int kSlotG = 9;
+constexpr int kSlot = 16 * kSlotG;
+constexpr int kBufLds = 64 * kSlot; // one tile image, 9 KiB
 constexpr int kBodyWaves = kBodyThreads / 64;
-static_assert(kBodyWaves * 2 * kWaveLds <= 160 * 1024, "two tile buffers per wave must fit the CU's LDS");
+constexpr int kBodyWgPerCu = 2;
+static_assert(kBodyWgPerCu * kBodyWaves * 2 * kBufLds <= 160 * 1024, "two tile buffers per wave must fit");
 
 typedef __attribute__((address_space(3))) void LdsVoid;
 typedef __attribute__((address_space(1))) void GVoid;
@@ -682,16 +678,15 @@ __device__ __forceinline__ uint32_t byte_mask_below(int e, int k) // bytes [4k, 
 }
 
 // The frame records a lane of the next tile loads (one batch of independent
-// dwordx4 loads, issued a full compute phase before they are used).  Kept
-// as raw granules so that nothing here becomes a private-memory copy.
+// dwordx4 loads, issued a compute window before they are used).  Kept as
+// raw granules so that nothing here becomes a private-memory copy.
 struct TileRecords {
     u32x4 h[6]; // FrameHot
     u32x4 p[7]; // FramePow
-    u32x4 f[4]; // FrameFin
     unsigned long long ex; // decode: replay-scan exclusive max
-    uint32_t last, sid;    // decode: last frame of its session / its session
+    unsigned long long psnap; // decode: session peer nonce before the batch
 };
-static_assert(sizeof(FrameHot) == 6 * 16 && sizeof(FramePow) == 7 * 16 && sizeof(FrameFin) == 4 * 16, "records");
+static_assert(sizeof(FrameHot) == 6 * 16 && sizeof(FramePow) == 7 * 16, "records");
 
 // Unconditional loads (an idle lane reads frame 0's records and ignores
 // them): a conditional load would need a register copy at the branch join,
@@ -699,27 +694,21 @@ static_assert(sizeof(FrameHot) == 6 * 16 && sizeof(FramePow) == 7 * 16 && sizeof
 template <bool DEC>
 __device__ __forceinline__ void load_records(TileRecords &R, uint32_t i, const FrameHot *__restrict__ hot,
                                              const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
-                                             const unsigned long long *__restrict__ excl,
-                                             const uint8_t *__restrict__ last, const uint32_t *__restrict__ sid)
+                                             const unsigned long long *__restrict__ excl)
 {
-    const GCU4 *ph = (const GCU4 *) (hot + i), *pp = (const GCU4 *) (pw + i), *pf = (const GCU4 *) (fin + i);
+    const GCU4 *ph = (const GCU4 *) (hot + i), *pp = (const GCU4 *) (pw + i);
 #pragma unroll
     for (int q = 0; q < 6; ++q)
         R.h[q] = ph[q];
 #pragma unroll
     for (int q = 0; q < 7; ++q)
         R.p[q] = pp[q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        R.f[q] = pf[q];
     if (DEC) {
         R.ex = excl[i];
-        R.last = last[i];
-        R.sid = sid[i];
+        R.psnap = fin[i].peer_snap;
     } else {
         R.ex = 0;
-        R.last = 0;
-        R.sid = 0;
+        R.psnap = 0;
     }
 }
 
@@ -727,6 +716,18 @@ template <int W>
 __device__ __forceinline__ uint32_t rec_word(const u32x4 *g)
 {
     return (W & 3) == 0 ? g[W >> 2].x : (W & 3) == 1 ? g[W >> 2].y : (W & 3) == 2 ? g[W >> 2].z : g[W >> 2].w;
+}
+
+template <int W>
+__device__ __forceinline__ fe rec_fe(const u32x4 *g)
+{
+    fe x;
+    x.l[0] = rec_word<W>(g);
+    x.l[1] = rec_word<W + 1>(g);
+    x.l[2] = rec_word<W + 2>(g);
+    x.l[3] = rec_word<W + 3>(g);
+    x.l[4] = rec_word<W + 4>(g);
+    return x;
 }
 
 // Per-lane state of one tile from its setup to its finish (plain words only).
@@ -743,30 +744,25 @@ struct TileLane {
     uint32_t k[8], n0, n1, r[5], nch, flags; // from FrameHot
     int32_t status;
     uint64_t out_base;
-    uint32_t hh[5], s[4], tag[4], wire_len; // from FrameFin
-    uint64_t peer_snap;
-    unsigned long long ex;
-    uint32_t last, sid;
 };
 
+// Sets up tile lane T from its frame's records and returns the chunk's
+// input stream address (for the DMA).
 template <bool DEC>
-__device__ __forceinline__ void tile_setup(TileLane &T, const TileRecords &R, bool valid, const FrameLook &lk,
-                                           uint32_t g, const uint32_t *__restrict__ powtab, uint8_t *buf)
+__device__ __forceinline__ uint64_t tile_setup(TileLane &T, const TileRecords &R, bool valid, const FrameLook &lk,
+                                               uint32_t g, const uint32_t *__restrict__ powtab)
 {
     const uint32_t lane = threadIdx.x & 63;
-    // Every loaded granule counts as used from here on: a record word that
-    // is never read would free its register while the load is in flight, and
-    // the next write to that register would wait for the load.
+    // every loaded granule counts as used from here on: a record word that
+    // is never read would free its register while the load is in flight,
+    // and the next write to that register would wait for the load
 #pragma unroll
     for (int q = 0; q < 6; ++q)
         asm volatile("" ::"v"(R.h[q]));
 #pragma unroll
     for (int q = 0; q < 7; ++q)
         asm volatile("" ::"v"(R.p[q]));
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        asm volatile("" ::"v"(R.f[q]));
-    asm volatile("" ::"v"(R.ex), "v"(R.last), "v"(R.sid));
+    asm volatile("" ::"v"(R.ex), "v"(R.psnap));
     // FrameHot words: key 0-7, r 8-12, nch 13, mlen 14, hl 15, n0 16, n1 17,
     // status 18, flags 19, in_base 20-21, out_base 22-23
     T.k[0] = rec_word<0>(R.h);
@@ -790,25 +786,6 @@ __device__ __forceinline__ void tile_setup(TileLane &T, const TileRecords &R, bo
     T.flags = rec_word<19>(R.h);
     const uint64_t in_base = ((uint64_t) rec_word<21>(R.h) << 32) | rec_word<20>(R.h);
     T.out_base = ((uint64_t) rec_word<23>(R.h) << 32) | rec_word<22>(R.h);
-    // FrameFin words: hh 0-4, s 5-8, tag 9-12, wire_len 13, peer_snap 14-15
-    T.hh[0] = rec_word<0>(R.f);
-    T.hh[1] = rec_word<1>(R.f);
-    T.hh[2] = rec_word<2>(R.f);
-    T.hh[3] = rec_word<3>(R.f);
-    T.hh[4] = rec_word<4>(R.f);
-    T.s[0] = rec_word<5>(R.f);
-    T.s[1] = rec_word<6>(R.f);
-    T.s[2] = rec_word<7>(R.f);
-    T.s[3] = rec_word<8>(R.f);
-    T.tag[0] = rec_word<9>(R.f);
-    T.tag[1] = rec_word<10>(R.f);
-    T.tag[2] = rec_word<11>(R.f);
-    T.tag[3] = rec_word<12>(R.f);
-    T.wire_len = rec_word<13>(R.f);
-    T.peer_snap = ((uint64_t) rec_word<15>(R.f) << 32) | rec_word<14>(R.f);
-    T.ex = R.ex;
-    T.last = R.last;
-    T.sid = R.sid;
 
     uint64_t src = 0;
     T.key = kIdle;
@@ -823,11 +800,11 @@ __device__ __forceinline__ void tile_setup(TileLane &T, const TileRecords &R, bo
         T.key = i;
         T.g0 = lk.ce - T.nch; // chunk_end[i - 1]
         T.c = g - T.g0;
-        const uint32_t P0 = 32 + 256 * T.c; // first plaintext byte of this chunk
-        uint32_t L = mlen > P0 ? (mlen - P0 < 256 ? mlen - P0 : 256) : 0;
+        const uint32_t P0 = 32 + kChunk * T.c; // first plaintext byte of this chunk
+        uint32_t L = mlen > P0 ? (mlen - P0 < kChunk ? mlen - P0 : kChunk) : 0;
         if (DEC) {
             const uint64_t nc = ((uint64_t) bswap32(T.n0) << 32) | bswap32(T.n1);
-            if (T.status != 0 || !sequence_ok(nc, T.peer_snap, T.ex))
+            if (T.status != 0 || !sequence_ok(nc, R.psnap, R.ex))
                 L = 0;
             src = in_base + 32 + P0;     // ciphertext byte P0 on the wire
             T.dst = T.out_base + P0 - 1; // plaintext byte P0 = payload byte P0-1
@@ -838,36 +815,19 @@ __device__ __forceinline__ void tile_setup(TileLane &T, const TileRecords &R, bo
         T.L = L;
         T.di = (uint32_t) (src & 15);
         if (L > 0 && T.c + 1 < T.nch) {
-            // chunk_factor from the raw FramePow record: r^blast * (r^16)^(nch-2-c)
-            // (words: rb 0-4, t[k] 5+5k .. 9+5k)
-            f.l[0] = rec_word<0>(R.p);
-            f.l[1] = rec_word<1>(R.p);
-            f.l[2] = rec_word<2>(R.p);
-            f.l[3] = rec_word<3>(R.p);
-            f.l[4] = rec_word<4>(R.p);
-            const uint32_t m = T.nch - 2 - T.c;
-            fe t;
-            if (m & 1) {
-                t.l[0] = rec_word<5>(R.p); t.l[1] = rec_word<6>(R.p); t.l[2] = rec_word<7>(R.p);
-                t.l[3] = rec_word<8>(R.p); t.l[4] = rec_word<9>(R.p);
-                fe_mul(f, t);
-            }
-            if (m & 2) {
-                t.l[0] = rec_word<10>(R.p); t.l[1] = rec_word<11>(R.p); t.l[2] = rec_word<12>(R.p);
-                t.l[3] = rec_word<13>(R.p); t.l[4] = rec_word<14>(R.p);
-                fe_mul(f, t);
-            }
-            if (m & 4) {
-                t.l[0] = rec_word<15>(R.p); t.l[1] = rec_word<16>(R.p); t.l[2] = rec_word<17>(R.p);
-                t.l[3] = rec_word<18>(R.p); t.l[4] = rec_word<19>(R.p);
-                fe_mul(f, t);
-            }
-            if (m & 8) {
-                t.l[0] = rec_word<20>(R.p); t.l[1] = rec_word<21>(R.p); t.l[2] = rec_word<22>(R.p);
-                t.l[3] = rec_word<23>(R.p); t.l[4] = rec_word<24>(R.p);
-                fe_mul(f, t);
-            }
+            // r^(Poly1305 blocks after this chunk) = r^blast * (r^8)^(nch-2-c)
+            // (FramePow words: rb 0-4, t[k] = r^(8*2^k) at 5+5k)
             static_assert(kPowInline == 4, "inline powers");
+            f = rec_fe<0>(R.p);
+            const uint32_t m = T.nch - 2 - T.c;
+            if (m & 1)
+                fe_mul(f, rec_fe<5>(R.p));
+            if (m & 2)
+                fe_mul(f, rec_fe<10>(R.p));
+            if (m & 4)
+                fe_mul(f, rec_fe<15>(R.p));
+            if (m & 8)
+                fe_mul(f, rec_fe<20>(R.p));
             const uint32_t *pt = powtab + (size_t) i * kMaxPow * 5;
             for (int k = kPowInline; (m >> k) != 0; ++k)
                 if ((m >> k) & 1)
@@ -879,45 +839,90 @@ __device__ __forceinline__ void tile_setup(TileLane &T, const TileRecords &R, bo
         T.f[q] = f.l[q];
     const uint32_t kn = __shfl_down(T.key, 1);
     T.Ln = __shfl_down(T.L, 1);
-    T.cont = (lane < 63 && T.key != kIdle && kn == T.key && T.L == 256 && T.Ln > 0) ? 1u : 0u;
+    T.cont = (lane < 63 && T.key != kIdle && kn == T.key && T.L == kChunk && T.Ln > 0) ? 1u : 0u;
     T.prevcont = (__shfl_up(T.cont, 1) != 0 && lane > 0) ? 1u : 0u;
-    ChunkParam p;
-    p.src = src;
-    p.dst = T.dst;
-    p.L = T.L;
-    p.cont = T.cont;
-    ((ChunkParam *) (buf + 64 * kSlot))[lane] = p;
+    return src;
 }
 
-// Coalesced LDS-DMA of a tile's input images into `buf` (no wait).
-__device__ __forceinline__ void tile_dma(uint8_t *buf)
+// Chunk parameters of the cooperative rounds: in round k lane l moves
+// granule q of chunk s, idx = 64k + l = kSlotG*s + q.  The rounds go in
+// groups of kGroup: the group's chunk addresses and lengths are fetched from
+// the owning lanes (ds_bpermute) together, so the rounds are not serialised
+// on LDS latency, while the registers they need stay bounded.
+constexpr uint32_t kGroup = 3;
+static_assert(kSlotG % kGroup == 0, "round groups");
+
+struct RoundParams {
+    uint64_t a[kGroup]; // chunk stream byte 0 (input or output)
+    uint32_t L[kGroup]; // chunk stream bytes
+    uint32_t q[kGroup]; // granule of the chunk this lane moves
+};
+
+__device__ __forceinline__ void round_params(RoundParams &P, uint32_t k0, uint64_t addr, uint32_t L)
 {
-    const uint32_t lane = threadIdx.x & 63;
-    const ChunkParam *prm = (const ChunkParam *) (buf + 64 * kSlot);
-    wave_lds_fence();
-#pragma unroll 1
-    for (uint32_t k = 0; k < 17; ++k) {
-        const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
-        const uint64_t ps = prm[s].src;
-        const uint32_t pL = prm[s].L;
-        const uint32_t off = (uint32_t) (ps & 15);
-        if (pL && q < ((off + pL + 15) >> 4))
-            __builtin_amdgcn_global_load_lds((GVoid *) (uintptr_t) ((ps - off) + 16 * q),
-                                             (LdsVoid *) (buf + 1024 * k), 16, 0, 0);
+    uint32_t ln = threadIdx.x & 63;
+    asm volatile("" : "+v"(ln)); // keep the round arithmetic out of the loop-invariant set
+    const uint32_t alo = (uint32_t) addr, ahi = (uint32_t) (addr >> 32);
+#pragma unroll
+    for (uint32_t j = 0; j < kGroup; ++j) {
+        const uint32_t idx = (k0 + j) * 64 + ln, s = idx / kSlotG;
+        P.q[j] = idx - kSlotG * s;
+        P.a[j] = ((uint64_t) (uint32_t) __shfl(ahi, (int) s) << 32) | (uint32_t) __shfl(alo, (int) s);
+        P.L[j] = (uint32_t) __shfl(L, (int) s);
+    }
+}
+
+// Coalesced LDS-DMA of a tile's input images into buf (no wait).
+__device__ __forceinline__ void tile_dma(uint8_t *buf, uint64_t src, uint32_t L)
+{
+#pragma unroll
+    for (uint32_t k0 = 0; k0 < kSlotG; k0 += kGroup) {
+        RoundParams P;
+        round_params(P, k0, src, L);
+#pragma unroll
+        for (uint32_t j = 0; j < kGroup; ++j) {
+            const uint32_t off = (uint32_t) (P.a[j] & 15);
+            if (P.L[j] && P.q[j] < ((off + P.L[j] + 15) >> 4))
+                __builtin_amdgcn_global_load_lds((GVoid *) (uintptr_t) ((P.a[j] - off) + 16 * P.q[j]),
+                                                 (LdsVoid *) (buf + 1024 * (k0 + j)), 16, 0, 0);
+        }
+    }
+}
+
+// Coalesced stores of a tile's interior output granules from buf: the
+// whole granules of each chunk's output image (an edge granule, shared with
+// a neighbour or partial, is stored by its lane).
+__device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t dst, uint32_t L)
+{
+#pragma unroll
+    for (uint32_t k0 = 0; k0 < kSlotG; k0 += kGroup) {
+        RoundParams P;
+        round_params(P, k0, dst, L);
+        u32x4 g[kGroup];
+#pragma unroll
+        for (uint32_t j = 0; j < kGroup; ++j)
+            g[j] = *(const u32x4 *) (buf + 16 * ((k0 + j) * 64 + (threadIdx.x & 63)));
+#pragma unroll
+        for (uint32_t j = 0; j < kGroup; ++j) {
+            const uint32_t pO = (uint32_t) (P.a[j] & 15);
+            const uint32_t qfirst = pO ? 1u : 0u;                         // granule 0 is an edge when misaligned
+            if (P.L[j] && P.q[j] >= qfirst && 16 * P.q[j] + 16 <= pO + P.L[j]) // whole granule inside the chunk
+                *(GU4 *) (uintptr_t) ((P.a[j] - pO) + 16 * P.q[j]) = g[j];
+        }
     }
 }
 
 template <bool DEC>
-__global__ __launch_bounds__(kBodyThreads) void k_body(
+__global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_body(
     uint32_t n, const uint32_t *__restrict__ chunk_end, const FrameHot *__restrict__ hot,
     const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin, const uint32_t *__restrict__ powtab,
     uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out, const uint32_t *__restrict__ sid,
     uint32_t max_sessions, unsigned long long *__restrict__ peer, unsigned long long *__restrict__ acc,
     uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl, const uint8_t *__restrict__ last)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kWaveLds];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kBufLds];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint8_t *const wlds = lds + wv * 2 * kWaveLds;
+    uint8_t *const wlds = lds + wv * 2 * kBufLds;
     const uint32_t total = chunk_end[n - 1];
     const uint64_t tiles = (total + 63) >> 6;
     const uint64_t W = (uint64_t) blockIdx.x * kBodyWaves + wv, NW = (uint64_t) gridDim.x * kBodyWaves;
@@ -934,9 +939,9 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
         const uint32_t g = 64 * tb + lane;
         const FrameLook lk = window_find(window_load(chunk_end, n, lo), lo, n, g);
         TileRecords R;
-        load_records<DEC>(R, g < total ? lk.i : 0, hot, pw, fin, excl, last, sid);
-        tile_setup<DEC>(cur, R, g < total, lk, g, powtab, wlds);
-        tile_dma(wlds);
+        load_records<DEC>(R, g < total ? lk.i : 0, hot, pw, fin, excl);
+        const uint64_t src = tile_setup<DEC>(cur, R, g < total, lk, g, powtab);
+        tile_dma(wlds, src, cur.L);
         if (tb + 1 < te) {
             const uint32_t lo1 = next_tile_lo(lk, 64 * (tb + 1));
             lkn = window_find(window_load(chunk_end, n, lo1), lo1, n, 64 * (tb + 1) + lane);
@@ -949,19 +954,36 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
         unsigned long long st_[8];
 #endif
         ZSTAMP(0);
-        uint8_t *const cb = wlds + ((t - tb) & 1) * kWaveLds;
-        uint8_t *const nb = wlds + (((t - tb) & 1) ^ 1) * kWaveLds;
+        uint8_t *const cb = wlds + ((t - tb) & 1) * kBufLds;
+        uint8_t *const nb = wlds + (((t - tb) & 1) ^ 1) * kBufLds;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile t's DMA (and everything before it)
         wave_lds_fence();
         ZSTAMP(1);
-        const bool has_next = t + 1 < te, has_next2 = t + 2 < te;
+        const bool has_next = t + 1 < te;
         // ---- issue: next tile's records, the chunk-end window after it
         const uint32_t gn = 64 * (t + 1) + lane;
         TileRecords Rn;
-        load_records<DEC>(Rn, has_next && gn < total ? lkn.i : 0, hot, pw, fin, excl, last, sid);
+        load_records<DEC>(Rn, has_next && gn < total ? lkn.i : 0, hot, pw, fin, excl);
         // (unconditional: on the last two tiles this reads a clamped, unused window)
         const uint32_t lo2 = next_tile_lo(lkn, 64 * (t + 2));
         const uint32_t ce2 = window_load(chunk_end, n, lo2 < n ? lo2 : n - 1);
+        // ---- issue: this tile's finish inputs (used after its stores, so that
+        // waiting for them does not wait for the stores)
+        u32x4 Fq[4];
+        uint32_t f_last = 0, f_sid = 0;
+        unsigned long long f_ex = 0;
+        {
+            const uint32_t fi = cur.key != kIdle ? cur.key : 0;
+            const GCU4 *pf = (const GCU4 *) (fin + fi);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                Fq[q] = pf[q];
+            if (DEC) {
+                f_last = last[fi];
+                f_sid = sid[fi];
+                f_ex = excl[fi];
+            }
+        }
         // ---- compute: keystream, MAC, output image (in place, one window behind)
         uint64_t v[5] = {0, 0, 0, 0, 0};
         const uint32_t L = cur.L, nwin = (L + 63) >> 6;
@@ -985,11 +1007,6 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 w[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], si);
-            if (tw + 1 < nwin) { // read ahead before this window's output overwrites it
-#pragma unroll
-                for (int q = 0; q < 17; ++q)
-                    d[q] = inw[16 * (tw + 1) + q];
-            }
             if (nv < 64)
                 mask_tail(w, nv);
 #if ZMQG_ABLATE == 2 // timing experiment only: memory traffic without keystream/MAC work
@@ -997,7 +1014,7 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
             for (int q = 0; q < 16; ++q)
                 ks[q] = tw * 16 + q;
 #else
-            salsa20_block(ks, cur.k, cur.n0, cur.n1, 1 + 4 * cur.c + tw, 0);
+            salsa20_block(ks, cur.k, cur.n0, cur.n1, 1 + 2 * cur.c + tw, 0);
 #endif
             if (DEC && ZMQG_ABLATE != 2)
                 poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
@@ -1011,6 +1028,11 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
 #if ZMQG_ABLATE == 2
             h.l[0] ^= w[0];
 #endif
+            if (tw + 1 < nwin) { // read ahead before this window's output overwrites it
+#pragma unroll
+                for (int q = 0; q < 17; ++q)
+                    d[q] = inw[16 * (tw + 1) + q];
+            }
             // image dword (dO>>2) + 16tw + q holds stream bytes [64tw + 4q - so, +4)
             if (so == 0) {
 #pragma unroll
@@ -1026,21 +1048,20 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
                     outw[16 * tw + 16] = __builtin_amdgcn_alignbyte(0u, w[15], 4 - so);
             }
         };
-        const uint32_t nw1 = nwin < 2 ? nwin : 2;
-        for (uint32_t tw = 0; tw < nw1; ++tw)
-            window(tw);
+        if (nwin > 0)
+            window(0);
         ZSTAMP(2);
         // ---- setup: next tile's params and its DMA; locate the tile after it
         // (on the wave's last tile this sets up an all-idle tile: no DMA)
         TileLane nx;
-        tile_setup<DEC>(nx, Rn, has_next && gn < total, lkn, gn, powtab, nb);
-        tile_dma(nb);
-        FrameLook lk2 = {kIdle, 0};
-        if (has_next2)
-            lk2 = window_find(ce2, lo2, n, 64 * (t + 2) + lane);
+        {
+            const uint64_t nsrc = tile_setup<DEC>(nx, Rn, has_next && gn < total, lkn, gn, powtab);
+            tile_dma(nb, nsrc, nx.L);
+        }
+        const FrameLook lk2 = window_find(ce2, lo2, n, 64 * (t + 2) + lane);
         ZSTAMP(3);
-        for (uint32_t tw = 2; tw < nwin; ++tw)
-            window(tw);
+        if (nwin > 1)
+            window(1);
         if (L > 0) {
             fe_mul(h, load_fe(cur.f));
 #pragma unroll
@@ -1050,20 +1071,9 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
         wave_lds_fence();
         ZSTAMP(4);
         // ---- store: coalesced interior granules, then this lane's edges
-        {
-            const ChunkParam *prm = (const ChunkParam *) (cb + 64 * kSlot);
-#pragma unroll 1
-            for (uint32_t k = 0; k < 17; ++k) {
-                const uint32_t idx = k * 64 + lane, s = idx / 17, q = idx - 17 * s;
-                const uint64_t pd = prm[s].dst;
-                const uint32_t pL = prm[s].L;
-                const uint32_t pO = (uint32_t) (pd & 15);
-                const uint32_t qfirst = pO ? 1u : 0u;          // granule 0 is an edge when misaligned
-                if (pL && q >= qfirst && 16 * q + 16 <= pO + pL) // whole granule inside the chunk
-                    *(GU4 *) (uintptr_t) ((pd - pO) + 16 * q) = *(const u32x4 *) (cb + 16 * idx);
-            }
-        }
-        if (L > 0) {
+        if (ZMQG_ABLATE != 5) // (timing experiments only)
+            tile_store_interior(cb, cur.dst, L);
+        if (L > 0 && ZMQG_ABLATE != 3) {
             const uint32_t end = dO + L;
             GU8 *gbase = (GU8 *) (uintptr_t) (cur.dst - dO);
             const uint32_t ql = end >> 4, el = end & 15; // granule of the last byte / its valid bytes
@@ -1093,48 +1103,58 @@ __global__ __launch_bounds__(kBodyThreads) void k_body(
         }
         ZSTAMP(5);
         // ---- finish: Poly1305 combine and tag / status
-        if (wave_segment_sum(cur.key, v)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            asm volatile("" ::"v"(Fq[q])); // (see tile_setup: keep every loaded word's register)
+        asm volatile("" ::"v"(f_last), "v"(f_sid), "v"(f_ex));
+        if (ZMQG_ABLATE != 4 && wave_segment_sum(cur.key, v)) {
             const uint32_t i = cur.key;
             if (frame_combine(cur.g0, cur.nch, acc + (size_t) i * 5, cnt + i, v)) {
+                // FrameFin words: hh 0-4, s 5-8, tag 9-12, wire_len 13, peer_snap 14-15
+                const fe hh = rec_fe<0>(Fq);
+                const uint32_t fs[4] = {rec_word<5>(Fq), rec_word<6>(Fq), rec_word<7>(Fq), rec_word<8>(Fq)};
                 if (!DEC) {
 #pragma unroll
                     for (int q = 0; q < 5; ++q)
-                        v[q] += cur.hh[q];
+                        v[q] += hh.l[q];
                     uint32_t tag[16];
-                    poly_finish(fe_from_wide(v), cur.s, tag);
+                    poly_finish(fe_from_wide(v), fs, tag);
                     store_window((uint8_t *) (uintptr_t) cur.out_base + 16, 16, tag);
                 } else {
+                    const uint32_t wtag[4] = {rec_word<9>(Fq), rec_word<10>(Fq), rec_word<11>(Fq), rec_word<12>(Fq)};
+                    const uint32_t wire_len = rec_word<13>(Fq);
+                    const unsigned long long psnap = ((uint64_t) rec_word<15>(Fq) << 32) | rec_word<14>(Fq);
                     int32_t status = cur.status;
-                    const unsigned long long ex = cur.ex;
+                    const unsigned long long ex = f_ex;
                     const uint64_t nc = ((uint64_t) bswap32(cur.n0) << 32) | bswap32(cur.n1);
-                    if (status == 0 && !sequence_ok(nc, cur.peer_snap, ex))
+                    if (status == 0 && !sequence_ok(nc, psnap, ex))
                         status = ZMQG_ERR_INVALID_SEQUENCE;
                     if (status == 0) {
 #pragma unroll
                         for (int q = 0; q < 5; ++q)
-                            v[q] += cur.hh[q];
+                            v[q] += hh.l[q];
                         uint32_t tag[4];
-                        poly_finish(fe_from_wide(v), cur.s, tag);
-                        const uint32_t diff = (tag[0] ^ cur.tag[0]) | (tag[1] ^ cur.tag[1]) | (tag[2] ^ cur.tag[2]) |
-                                              (tag[3] ^ cur.tag[3]);
+                        poly_finish(fe_from_wide(v), fs, tag);
+                        const uint32_t diff =
+                            (tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]);
                         if (diff)
                             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
                     }
                     status_out[i] = status;
                     flags_out[i] = status == 0 ? (uint8_t) cur.flags : 0;
-                    if (status != 0 && cur.wire_len >= 33) {
+                    if (status != 0 && wire_len >= 33) {
                         uint8_t *o = (uint8_t *) (uintptr_t) cur.out_base;
-                        for (uint32_t b = 0; b < cur.wire_len - 33; ++b)
+                        for (uint32_t b = 0; b < wire_len - 33; ++b)
                             o[b] = 0;
                     }
-                    if (cur.last) {
+                    if (f_last) {
                         // _cn_peer_nonce after the batch: max over accepted headers
-                        unsigned long long p = cur.peer_snap;
+                        unsigned long long p = psnap;
                         if (ex > p)
                             p = ex;
                         if (cur.status == 0 && nc > p)
                             p = nc;
-                        peer[cur.sid < max_sessions ? cur.sid : 0] = p;
+                        peer[f_sid < max_sessions ? f_sid : 0] = p;
                     }
                 }
             }
@@ -1220,8 +1240,8 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
 
 uint32_t body_grid(const zmqg_ctx *ctx)
 {
-    // persistent: one workgroup (4 waves, one per SIMD) per compute unit
-    return ctx->cus > 0 ? (uint32_t) ctx->cus : 256u;
+    // persistent: kBodyWgPerCu workgroups of 4 waves per compute unit
+    return kBodyWgPerCu * (ctx->cus > 0 ? (uint32_t) ctx->cus : 256u);
 }
 
 int check_n(uint64_t n)

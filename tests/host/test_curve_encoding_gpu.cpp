@@ -96,7 +96,7 @@ int main ()
           0x07, 0x4d, 0x45, 0x53, 0x53, 0x41, 0x47, 0x45, 0, 0, 0, 0,
           0,    0,    0,    1,    0x21, 0x1a, 0xc2, 0x5d, 0x7f, 0xfe, 0x52, 0x01,
           0xb4, 0x38, 0x80, 0xd3, 0xfb, 0x29, 0xfb, 0x06, 0x94, 0xb7, 0x29, 0x81};
-        CHECK (m.size () == 1024 + 34);
+        CHECK (m.size () == 1024 + 33);
         CHECK (memcmp (m.data (), want, 36) == 0);
         ++tests_run;
     }
@@ -140,6 +140,9 @@ int main ()
             sv.push_back (new zmqg::curve_encoding_gpu_t (ctx, 4 + c, server_prefix, client_prefix, c == 2));
             fill_precom (cl[c]->get_writable_precom_buffer (), 100 + c);
             memcpy (sv[c]->get_writable_precom_buffer (), cl[c]->get_precom_buffer (), 32);
+            // the first MESSAGE nonce here is 1: reset the peer nonce as the
+            // reference's unittest does (no handshake advanced it)
+            sv[c]->set_peer_nonce (0);
         }
         const int n = 30;
         std::vector<zmqg::msg_buf_t> msgs (n);

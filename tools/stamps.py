@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Phase breakdown of the body kernel from a ZMQG_STAMPS build (diagnostic).
-Stamps (s_memtime ticks, relative to iteration start): 1 tile's DMA
-waited for, 2 compute windows 0-1 done, 3 next tile set up and its DMA
-issued, 4 compute windows 2-3 done, 5 output stores issued, 6 finish done."""
+Stamps (s_memtime ticks, relative to tile start): 1 setup done, 2 phase-0
+input landed in LDS, 3 phase-0 compute done, 4 phase-0 stores issued,
+5 phase 1 (DMA, compute, stores) done, 6 finish done."""
 import ctypes
 import os
 import subprocess
@@ -24,7 +24,7 @@ cnt = ctypes.c_uint32(0)
 assert L.zmqg_debug_stamps(buf, 16384, ctypes.byref(cnt)) == 0
 a = np.frombuffer(buf, np.uint64)[: cnt.value * 8].reshape(-1, 8)[:, :7].astype(np.float64)
 print("records", cnt.value)
-names = ["wait", "compute1", "setupnext", "compute2", "stores", "finish"]
+names = ["wait", "window0", "setupnext", "window1", "stores", "finish"]
 d = np.diff(a, axis=1)
 for k, nme in enumerate(names):
     print(f"  {nme:8s} mean {d[:, k].mean():9.0f}  p50 {np.median(d[:, k]):9.0f}  p90 {np.percentile(d[:, k], 90):9.0f} ticks")
