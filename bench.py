@@ -148,15 +148,21 @@ def main():
     enc_avg_s = enc_body_ms / max(enc_body_n, 1) / 1e3
     dec_read = n * (P + 49)
     achieved = dec_read / dec_avg_s / 1e9 if dec_avg_s > 0 else None
-    traffic = None
+    # traffic: HBM read bytes per launch of the same kernel from the committed
+    # PMC pass (FETCH_SIZE, doubled per the gfx950 note in MI355X_MICROARCH.md);
+    # the write side is reported beside it
+    traffic = traffic_write = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic_config2.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and n == 65536 and P == 1024:
         try:
-            traffic = json.load(open(pmc)).get("k_decode_body_bytes_per_launch")
+            d = json.load(open(pmc))
+            traffic = d.get("k_decode_body_bytes_per_launch")
+            traffic_write = d.get("k_decode_body_write_bytes_per_launch")
         except Exception:
-            traffic = None
+            traffic = traffic_write = None
     roofline = {"bound": "hbm", "kernel": "k_decode_body", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None, "traffic": traffic,
+                "traffic_write": traffic_write,
                 "algorithmic_bytes_per_launch": dec_read, "avg_launch_us": dec_avg_s * 1e6,
                 "encode_body_avg_us": enc_avg_s * 1e6,
                 "encode_call_avg_us": enc_call_ms / max(enc_body_n, 1) * 1e3,
