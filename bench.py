@@ -14,7 +14,7 @@ frame with no data exchange (weak scaling).  Ranks meet only at the
 barriers around the timed region (gloo, control only).
 
 JSON line fields beyond the driver contract:
-  roofline      dominant kernel (decode body) achieved algorithmic HBM-read
+  roofline      dominant kernel (decode frame kernel) achieved algorithmic HBM-read
                 GB/s vs the 8 TB/s peak, durations from HIP events recorded
                 live around that kernel on its stream during the timed steps;
                 traffic = PMC-measured HBM bytes per launch from
@@ -37,6 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+ROOF_KERNEL = "k_frames<decode>"  # the dominant kernel of the bench workload
 
 
 def parse():
@@ -111,7 +112,8 @@ def main():
 
     enc.set_profiling(True)
     dec.set_profiling(True)
-    enc.get_profile(0), dec.get_profile(1)  # clear
+    for k in range(6):  # clear
+        enc.get_profile(k), dec.get_profile(k)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -127,8 +129,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    enc_body_ms, enc_body_n = enc.get_profile(C.CurveContext.PROF_ENCODE_BODY)
-    dec_body_ms, dec_body_n = dec.get_profile(C.CurveContext.PROF_DECODE_BODY)
+    enc_body_ms, enc_body_n = enc.get_profile(C.CurveContext.PROF_ENCODE_MAIN)
+    dec_body_ms, dec_body_n = dec.get_profile(C.CurveContext.PROF_DECODE_MAIN)
     enc_call_ms, _ = enc.get_profile(C.CurveContext.PROF_ENCODE_CALL)
     dec_call_ms, _ = dec.get_profile(C.CurveContext.PROF_DECODE_CALL)
     enc.set_profiling(False)
@@ -141,7 +143,7 @@ def main():
     value = gib / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
-    # roofline of the dominant kernel: decode body.  Algorithmic HBM-read
+    # roofline of the dominant kernel: the decode frame kernel.  Algorithmic HBM-read
     # bytes of decode per frame: wire W + sid 4 + offset 8 +
     # length 4 = P + 49.
     dec_avg_s = dec_body_ms / max(dec_body_n, 1) / 1e3
@@ -156,15 +158,16 @@ def main():
     if os.path.exists(pmc) and n == 65536 and P == 1024:
         try:
             d = json.load(open(pmc))
-            traffic = d.get("k_decode_body_bytes_per_launch")
-            traffic_write = d.get("k_decode_body_write_bytes_per_launch")
+            if d.get("kernel") == ROOF_KERNEL:
+                traffic = d.get("read_bytes_per_launch")
+                traffic_write = d.get("write_bytes_per_launch")
         except Exception:
             traffic = traffic_write = None
-    roofline = {"bound": "hbm", "kernel": "k_decode_body", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+    roofline = {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None, "traffic": traffic,
                 "traffic_write": traffic_write,
                 "algorithmic_bytes_per_launch": dec_read, "avg_launch_us": dec_avg_s * 1e6,
-                "encode_body_avg_us": enc_avg_s * 1e6,
+                "encode_main_avg_us": enc_avg_s * 1e6,
                 "encode_call_avg_us": enc_call_ms / max(enc_body_n, 1) * 1e3,
                 "decode_call_avg_us": dec_call_ms / max(dec_body_n, 1) * 1e3,
                 "path_read_frac": (n * (2 * P + 74)) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS * world

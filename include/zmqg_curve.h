@@ -140,14 +140,19 @@ int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
 
 /* Profiling hooks (off by default).  When enabled, the ctx records a HIP
  * event pair on the batch's stream around each of its kernels of one kind:
- *   ZMQG_PROF_ENCODE_BODY / ZMQG_PROF_DECODE_BODY  the body kernel alone,
- *   ZMQG_PROF_ENCODE_CALL / ZMQG_PROF_DECODE_CALL  the whole batch call.
+ *   ZMQG_PROF_ENCODE_MAIN / ZMQG_PROF_DECODE_MAIN  the frame kernel alone
+ *     (every frame up to 4.5 KiB of stream: the dominant kernel),
+ *   ZMQG_PROF_ENCODE_CALL / ZMQG_PROF_DECODE_CALL  the whole batch call,
+ *   ZMQG_PROF_ENCODE_BODY / ZMQG_PROF_DECODE_BODY  the chunked body kernel
+ *     (larger frames) alone.
  * zmqg_ctx_get_profile synchronises the device, returns the summed elapsed
  * milliseconds and launch count for `kind` since the last reset, and resets. */
-#define ZMQG_PROF_ENCODE_BODY 0
-#define ZMQG_PROF_DECODE_BODY 1
+#define ZMQG_PROF_ENCODE_MAIN 0
+#define ZMQG_PROF_DECODE_MAIN 1
 #define ZMQG_PROF_ENCODE_CALL 2
 #define ZMQG_PROF_DECODE_CALL 3
+#define ZMQG_PROF_ENCODE_BODY 4
+#define ZMQG_PROF_DECODE_BODY 5
 int zmqg_ctx_set_profiling(zmqg_ctx *ctx, int enable);
 int zmqg_ctx_get_profile(zmqg_ctx *ctx, int kind, double *ms_total, uint64_t *launches);
 

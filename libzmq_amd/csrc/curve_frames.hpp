@@ -1,0 +1,733 @@
+// curve_frames.hpp -- the frame kernel: whole CURVE MESSAGE frames (encode or
+// decode) in one pass, G lanes per frame.
+//
+// Reference: src/curve_mechanism_base.cpp:111-205 (encode) and :207-284
+// (decode, with check_validity :80-109 and mechanism_base.cpp:14-25), i.e.
+// libsodium 1.0.18 crypto_box_easy_afternm / crypto_box_open_easy_afternm on
+// one frame each.
+//
+// Stream image.  Stream byte j of a frame is keystream byte j: bytes 0..31
+// are the Poly1305 key area, byte 32+p is plaintext byte p.  On the wire,
+// stream byte j >= 32 is wire byte j (ciphertext), so encode's output stream
+// is the wire frame itself and decode's input stream is the wire frame; the
+// plaintext side is offset by the plaintext header (encode: flags byte and
+// sub/cancel prefix, src/curve_mechanism_base.cpp:118-164; decode: the flags
+// byte, :250-260).  A window is 64 stream bytes = one Salsa20 block = four
+// 16-byte Poly1305 blocks of ciphertext (window 0: two, the other two are
+// the key area).
+//
+// Work split.  The G lanes of a frame take windows w = q, q+G, q+2G, ...
+// (lane q), so each step a frame's G lanes read and write 64*G contiguous
+// bytes.  Lane 0 starts with window 0 (keystream block 0 -> Poly1305 r, s)
+// and hands r to its group by a shuffle.  Poly1305 is evaluated in parallel:
+// with virtual blocks v = ciphertext block + 2 (two leading zero blocks,
+// which do not change the MAC), window w holds v = 4w..4w+3, and for NV
+// virtual blocks and L = last window, k = NV - 4L blocks in it,
+//     h = sum_{w<L} r^(k + 4(L-1-w)) U_w + U'_L,
+//     U_w = sum_j m_{4w+j} r^(4-j),   U'_L = sum_{j<k} m_{4L+j} r^(k-j),
+// so lane q keeps H_q = H_q r^(4G) + U_w over its windows below L and scales
+// H_q by r^(k + 4(L-1-w_q)) at the end; the group sums the lanes' terms and
+// lane 0 finishes the tag (encode: writes it; decode: compares).
+//
+// Memory.  Loads and stores are 4-byte aligned dwordx4 (aligned 4-byte words
+// of arbitrarily aligned frames), shifted in registers with v_alignbyte; an
+// output dword straddling two windows is written by the later window, which
+// gets the earlier window's last word from the lane that computed it.  Only
+// the first output dword of a frame and its tail are byte-exact stores, so
+// neighbouring frames are never touched.
+#pragma once
+
+#include "../../include/zmqg_curve.h"
+#include "curve_device.hpp"
+
+namespace zmqg {
+
+struct DevSession {
+    uint32_t enc_key[8]; // HSalsa20(precom, enc_prefix)
+    uint32_t dec_key[8]; // HSalsa20(precom, dec_prefix)
+    uint32_t downgrade_sub;
+    uint32_t pad[7];
+};
+
+// plaintext header of src/curve_mechanism_base.cpp:118-158 as 3 words
+__device__ __forceinline__ uint32_t plaintext_header(uint32_t msg_flags, uint32_t downgrade, uint32_t hw[3])
+{
+    const uint32_t f = msg_flags & 3u; // more | command
+    const uint32_t ct = msg_flags & 0x1c;
+    const bool sub = ct == 12u, cancel = ct == 16u;
+    hw[1] = hw[2] = 0;
+    if (!(sub || cancel)) {
+        hw[0] = f;
+        return 1;
+    }
+    if (downgrade) {
+        hw[0] = f | ((sub ? 1u : 0u) << 8);
+        return 2;
+    }
+    if (cancel) { // f|2, "\x06CANCEL"
+        hw[0] = (f | 2u) | (6u << 8) | ((uint32_t) 'C' << 16) | ((uint32_t) 'A' << 24);
+        hw[1] = (uint32_t) 'N' | ((uint32_t) 'C' << 8) | ((uint32_t) 'E' << 16) | ((uint32_t) 'L' << 24);
+        return 8;
+    }
+    // f|2, "\x09SUBSCRIBE"
+    hw[0] = (f | 2u) | (9u << 8) | ((uint32_t) 'S' << 16) | ((uint32_t) 'U' << 24);
+    hw[1] = (uint32_t) 'B' | ((uint32_t) 'S' << 8) | ((uint32_t) 'C' << 16) | ((uint32_t) 'R' << 24);
+    hw[2] = (uint32_t) 'I' | ((uint32_t) 'B' << 8) | ((uint32_t) 'E' << 16);
+    return 11;
+}
+
+// out[i] = stream bytes of p shifted right by HL bytes (zeros shifted in), 8 words.
+template <int HL>
+__device__ __forceinline__ void shift_in(const uint32_t p[16], uint32_t out[8])
+{
+    constexpr int A = HL >> 2, B = HL & 3;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t hi = (i - A >= 0) ? p[i - A] : 0u;
+        const uint32_t lo = (i - A - 1 >= 0) ? p[i - A - 1] : 0u;
+        out[i] = B == 0 ? hi : __builtin_amdgcn_alignbyte(hi, lo, 4 - B);
+    }
+}
+
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+typedef __attribute__((address_space(1))) const u32x4_a4 GCU4a4;
+typedef __attribute__((address_space(1))) u32x4_a4 GU4a4;
+typedef __attribute__((address_space(1))) const uint32_t GCU32;
+
+// Raw aligned words for window w of a stream whose byte 0 is at A and whose
+// bytes [0, S) may be read: d[k] = the aligned word holding stream byte
+// 64w + 4k - (A & 3).  Fast path: four dwordx4 + one dword.  At the stream's
+// end only words that hold a stream byte < S are read (such a word never
+// crosses into a page the stream does not touch).
+__device__ __forceinline__ void frame_load_raw(uint64_t A, uint32_t w, uint32_t S, uint32_t d[17])
+{
+    const uint32_t v = (uint32_t) A & 3u;
+    const uint64_t a4 = (A & ~3ull) + 64ull * w;
+    if (64u * w + 68u <= S) {
+        const GCU4a4 *p = (const GCU4a4 *) (uintptr_t) a4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32x4 t = p[k];
+            d[4 * k] = t.x;
+            d[4 * k + 1] = t.y;
+            d[4 * k + 2] = t.z;
+            d[4 * k + 3] = t.w;
+        }
+        d[16] = *(GCU32 *) (uintptr_t) (a4 + 64);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 17; ++k)
+            d[k] = (64u * w + 4u * k < S + v) ? *(GCU32 *) (uintptr_t) (a4 + 4u * k) : 0u;
+    }
+}
+
+// Stream words of window w from the raw words (zero at and beyond S).
+__device__ __forceinline__ void frame_words(const uint32_t d[17], uint32_t v, uint32_t w, uint32_t S, uint32_t x[16])
+{
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        x[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], v);
+    if (S < 64u * w + 64u)
+        mask_tail(x, (int) (S - 64u * w));
+}
+
+// Store output stream words y of window w >= 1 (stream byte 0 at B): the 16
+// aligned words covering stream [64w - up, 64w + 64 - up), up = B&3 or 4,
+// word 0 completed with yprev (word 15 of window w-1); on the frame's last
+// window also the tail up to S.  Bytes >= S are never written.
+__device__ __forceinline__ void frame_store(uint64_t B, uint32_t w, uint32_t S, const uint32_t y[16], uint32_t yprev,
+                                            bool last)
+{
+    const uint32_t u = (uint32_t) B & 3u, up = u ? u : 4u, sh = 4u - up;
+    const uint64_t a = B - up + 64ull * w; // aligned
+    uint32_t o[17];
+    o[0] = __builtin_amdgcn_alignbyte(y[0], yprev, sh);
+#pragma unroll
+    for (int k = 1; k < 16; ++k)
+        o[k] = __builtin_amdgcn_alignbyte(y[k], y[k - 1], sh);
+    o[16] = __builtin_amdgcn_alignbyte(0u, y[15], sh);
+    if (64u * w + 64u <= S) {
+        GU4a4 *p = (GU4a4 *) (uintptr_t) a;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            p[k] = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+        if (last) { // S == 64w + 64: the last `up` bytes
+            GU8 *t = (GU8 *) (uintptr_t) (a + 64);
+            if (up == 4u) {
+                *(GU32 *) t = o[16];
+            } else {
+#pragma unroll
+                for (uint32_t b = 0; b < 3; ++b)
+                    if (b < up)
+                        t[b] = (uint8_t) (o[16] >> (8 * b));
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 17; ++k) {
+            const int s0 = (int) (64u * w + 4u * k) - (int) up; // stream byte of this word's byte 0
+            GU8 *t = (GU8 *) (uintptr_t) (a + 4u * k);
+            if (s0 + 4 <= (int) S) {
+                *(GU32 *) t = o[k];
+            } else if (s0 < (int) S) {
+                const int nb = (int) S - s0;
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    if (b < nb)
+                        t[b] = (uint8_t) (o[k] >> (8 * b));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- Poly1305, parallel form
+struct fe5 { // an element plus 5x its limbs 1..4 (the reduction multipliers)
+    fe e;
+    uint32_t s1, s2, s3, s4;
+};
+
+__device__ __forceinline__ fe5 fe5_of(const fe &x)
+{
+    fe5 r;
+    r.e = x;
+    r.s1 = x.l[1] * 5;
+    r.s2 = x.l[2] * 5;
+    r.s3 = x.l[3] * 5;
+    r.s4 = x.l[4] * 5;
+    return r;
+}
+
+// a += m * p (m: limbs of a block or an element, p: a power of r)
+__device__ __forceinline__ void acc_mul(uint64_t a[5], const uint32_t m[5], const fe5 &p)
+{
+    const uint32_t p0 = p.e.l[0], p1 = p.e.l[1], p2 = p.e.l[2], p3 = p.e.l[3], p4 = p.e.l[4];
+    a[0] = mad64(m[0], p0, mad64(m[1], p.s4, mad64(m[2], p.s3, mad64(m[3], p.s2, mad64(m[4], p.s1, a[0])))));
+    a[1] = mad64(m[0], p1, mad64(m[1], p0, mad64(m[2], p.s4, mad64(m[3], p.s3, mad64(m[4], p.s2, a[1])))));
+    a[2] = mad64(m[0], p2, mad64(m[1], p1, mad64(m[2], p0, mad64(m[3], p.s4, mad64(m[4], p.s3, a[2])))));
+    a[3] = mad64(m[0], p3, mad64(m[1], p2, mad64(m[2], p1, mad64(m[3], p0, mad64(m[4], p.s4, a[3])))));
+    a[4] = mad64(m[0], p4, mad64(m[1], p3, mad64(m[2], p2, mad64(m[3], p1, mad64(m[4], p0, a[4])))));
+}
+
+// limbs of the 16-byte block in words w[0..3] with the 2^128 bit (full block)
+// or, for a partial block of nb < 16 bytes (bytes >= nb already zero), the
+// 0x01 pad byte at nb and no 2^128 bit
+__device__ __forceinline__ void block_limbs(const uint32_t *w, int nb, uint32_t m[5])
+{
+    uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], hib = 1u << 24;
+    if (nb < 16) {
+        hib = 0;
+        const uint32_t pad = 1u << (8 * (nb & 3));
+        const int wi = nb >> 2;
+        w0 |= wi == 0 ? pad : 0u;
+        w1 |= wi == 1 ? pad : 0u;
+        w2 |= wi == 2 ? pad : 0u;
+        w3 |= wi == 3 ? pad : 0u;
+    }
+    m[0] = w0 & M26;
+    m[1] = __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
+    m[2] = __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
+    m[3] = __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
+    m[4] = (w3 >> 8) | hib;
+}
+
+// Replay rule of src/curve_mechanism_base.cpp:98-106 in the decode frame
+// kernel.  Per frame: the header-valid nonce vout (0 for a header failure)
+// and the session's peer nonce before the batch (psnap).
+//   One session (ticket != null): workgroups take their frames in ticket
+//   order and run a decoupled look-back over the workgroup maxima of vout,
+//   so each frame knows excl = max of every earlier header-valid nonce in
+//   the batch; small frames apply the rule here, big frames get excl for
+//   the body's finisher, and the last workgroup writes the new peer nonce.
+//   Several sessions (ticket == null): iota for the sort-by-session path;
+//   the rule is applied by k_fixup / the body finisher.
+struct ReplayOut {
+    unsigned long long *vout;
+    unsigned long long *psnap;
+    uint32_t *iota;
+    unsigned long long *peer; // read (psnap); one session: written by the last workgroup
+    unsigned long long *excl; // one session: per frame, for the body finisher
+    uint32_t *ticket;         // one session: this call's workgroup ticket counter
+    uint32_t *ticket_next;    // ... and the next call's (cleared here)
+    unsigned long long *lb_flag, *lb_agg, *lb_inc; // look-back state per ticket
+    uint32_t epoch;           // call number (look-back flags of older calls are stale)
+    uint32_t dbg;             // timing experiments only (tools/frames_bench): 1 no look-back, 2 no ticket
+};
+
+// Decoupled look-back, whole workgroup: maximum of the aggregates of every
+// workgroup ticket < t, reading 256 tickets per round (one per thread) and
+// stopping at the nearest one that has published its inclusive value.
+// Every earlier ticket has started (tickets are taken at workgroup start)
+// and publishes its aggregate right after its header pass, so the spin is
+// short; run right after this workgroup's own header pass, so inclusive
+// values appear in ticket order early in the kernel.
+__device__ __forceinline__ unsigned long long lookback_excl(uint32_t t, uint32_t epoch,
+                                                            const unsigned long long *lb_flag,
+                                                            const unsigned long long *lb_agg,
+                                                            const unsigned long long *lb_inc)
+{
+    __shared__ uint32_t sh_stop[4];
+    __shared__ unsigned long long sh_v[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    unsigned long long P = 0;
+    for (int base = (int) t; base > 0; base -= 256) {
+        const int k = base - 1 - (int) tid; // this thread's predecessor
+        int state = 2;                      // out of range: an inclusive zero
+        if (k >= 0) {
+            unsigned long long f;
+            do {
+                f = __hip_atomic_load(lb_flag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((uint32_t) (f >> 2) != epoch || (f & 3ull) == 0);
+            state = (int) (f & 3ull);
+        }
+        unsigned long long v = 0;
+        if (k >= 0)
+            v = __hip_atomic_load((state == 2 ? lb_inc : lb_agg) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long m = __ballot(state == 2);
+        if (lane == 0)
+            sh_stop[wv] = m ? 64u * wv + (uint32_t) __builtin_ctzll(m) : 256u;
+        __syncthreads();
+        uint32_t stop = 256;
+        for (int w = 0; w < 4; ++w)
+            stop = sh_stop[w] < stop ? sh_stop[w] : stop;
+        if (tid > stop)
+            v = 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const unsigned long long o = __shfl_xor(v, d);
+            v = o > v ? o : v;
+        }
+        if (lane == 0)
+            sh_v[wv] = v;
+        __syncthreads();
+        for (int w = 0; w < 4; ++w)
+            P = sh_v[w] > P ? sh_v[w] : P;
+        __syncthreads();
+        if (stop < 256)
+            break;
+    }
+    return P;
+}
+
+// Hand-off without fences (MI355X_MICROARCH.md, "Valid forms": write-through
+// sc1 stores drained by s_waitcnt vmcnt(0) before the flag, sc1 loads on the
+// reading side).  An agent-scope release would write back the whole XCD L2,
+// full of this kernel's output: tens of microseconds per workgroup.
+__device__ __forceinline__ void lookback_publish(unsigned long long *flag, unsigned long long *val,
+                                                 unsigned long long v, uint32_t epoch, uint32_t state)
+{
+    __hip_atomic_store(val, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, ((unsigned long long) epoch << 2) | state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// No big-frame handler (tools, tests): frames above max_stream are skipped.
+struct NoBigFrames {
+    __device__ void operator()(uint32_t) const {}
+};
+
+// Frame kernel.  DEC = decode.  Frames whose stream is longer than
+// max_stream (with a valid header, for decode) are handed to `big(i)` on
+// one lane (the chunked path's head: block 0, records, list entry).
+// Workgroup 0 clears *zero_next (the next call's big-frame list counter).
+template <bool DEC, int G, class BigOp>
+__global__ __launch_bounds__(256) void k_frames(
+    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
+    const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
+    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
+    uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
+    ReplayOut rp, BigOp big, unsigned long long *__restrict__ zero_next)
+{
+    static_assert(G == 1 || G == 2 || G == 4, "lanes per frame");
+    const bool lb = DEC && rp.ticket != nullptr;
+    uint32_t wg = blockIdx.x;
+    __shared__ uint32_t sh_ticket;
+    __shared__ unsigned long long sh_wmax[4];
+    if (lb && !(rp.dbg & 2)) {
+        if (threadIdx.x == 0)
+            sh_ticket = atomicAdd(rp.ticket, 1u);
+        __syncthreads();
+        wg = sh_ticket;
+    }
+    if (wg == 0 && threadIdx.x == 0) {
+        if (zero_next)
+            *zero_next = 0;
+        if (lb)
+            *rp.ticket_next = 0;
+    }
+    const uint32_t gl = wg * 256u + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t i = gl / G, q = gl % G;
+    const uint32_t gbase = lane - q; // the group's lane 0
+    const bool valid = i < n;
+    const uint32_t ii = valid ? i : n - 1;
+    const uint32_t s = sid[ii] < max_sessions ? sid[ii] : 0u;
+    const DevSession &ses = sessions[s];
+    uint32_t key[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        key[t] = DEC ? ses.dec_key[t] : ses.enc_key[t];
+    const uint8_t *src = in + in_off[ii];
+    uint8_t *dst = out + out_off[ii];
+    const uint32_t L_in = len[ii];
+
+    uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
+    uint64_t A = 0, B = 0;
+    int32_t status = 0;
+    uint32_t hw[3] = {0, 0, 0};
+    if (!DEC) {
+        const uint64_t nc = nonce[ii];
+        n0 = bswap32((uint32_t) (nc >> 32));
+        n1 = bswap32((uint32_t) nc);
+        hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
+        S = 32u + hl + L_in;
+        A = (uint64_t) (uintptr_t) src - 32u - hl;
+        B = (uint64_t) (uintptr_t) dst;
+    } else {
+        // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
+        uint32_t h16[16];
+        load_window(src, L_in < 16u ? (int) L_in : 16, h16);
+        const uint32_t b0 = h16[0] & 0xffu;
+        if (L_in <= 1u || L_in <= b0)
+            status = ZMQG_ERR_MALFORMED_UNSPECIFIED;
+        else if (L_in < 8u || h16[0] != 0x53454d07u || h16[1] != 0x45474153u)
+            status = ZMQG_ERR_UNEXPECTED_COMMAND;
+        else if (L_in < 33u)
+            status = ZMQG_ERR_MALFORMED_MESSAGE;
+        n0 = h16[2];
+        n1 = h16[3];
+        S = status == 0 ? L_in : 0u;
+        A = (uint64_t) (uintptr_t) src;
+        B = (uint64_t) (uintptr_t) dst - 33u;
+    }
+    const bool small = valid && S <= max_stream;
+    // decode replay bookkeeping: header-valid nonce (0 = not a candidate),
+    // its exclusive max-scan inside the workgroup (frame order = thread
+    // order), the workgroup aggregate published for the look-back
+    unsigned long long vn = 0, wexcl = 0, psn = 0, wagg = 0;
+    if (DEC) {
+        vn = valid && q == 0 && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
+        psn = rp.peer[s];
+        if (valid && q == 0) {
+            rp.vout[i] = vn;
+            rp.psnap[i] = psn;
+            if (rp.iota)
+                rp.iota[i] = i;
+        }
+        if (lb) {
+            unsigned long long sc = vn;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const unsigned long long o = __shfl_up(sc, d);
+                if ((int) lane >= d)
+                    sc = o > sc ? o : sc;
+            }
+            const unsigned long long up = __shfl_up(sc, 1);
+            if (lane == 63)
+                sh_wmax[threadIdx.x >> 6] = sc;
+            __syncthreads();
+            const uint32_t wv = threadIdx.x >> 6;
+            for (uint32_t k = 0; k < 4; ++k) {
+                if (k < wv)
+                    wexcl = sh_wmax[k] > wexcl ? sh_wmax[k] : wexcl;
+                wagg = sh_wmax[k] > wagg ? sh_wmax[k] : wagg;
+            }
+            if (lane > 0)
+                wexcl = up > wexcl ? up : wexcl;
+            if (threadIdx.x == 0)
+                lookback_publish(rp.lb_flag + wg, rp.lb_agg + wg, wagg, rp.epoch, 1);
+        }
+    }
+    // replay: this workgroup's exclusive prefix (every earlier frame's
+    // header-valid nonce) from the look-back, published as soon as known
+    unsigned long long excl = 0;
+    if (lb) {
+        const unsigned long long P =
+            (rp.dbg & 1) ? 0ull : lookback_excl(wg, rp.epoch, rp.lb_flag, rp.lb_agg, rp.lb_inc);
+        if (threadIdx.x == 0) {
+            const unsigned long long inc = P > wagg ? P : wagg;
+            lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, rp.epoch, 2);
+            if (wg + 1 == gridDim.x) // _cn_peer_nonce after the batch
+                *rp.peer = inc > psn ? inc : psn;
+        }
+        excl = P > wexcl ? P : wexcl;
+        if (excl < psn)
+            excl = psn;
+    }
+    const bool is_big = valid && !small && S > 0;
+    if (!small)
+        S = 0; // nothing for this lane
+    const uint32_t nw = (S + 63u) >> 6;
+    const uint32_t L = nw ? nw - 1 : 0;
+    const uint32_t kb = nw ? ((S - 64u * L + 15u) >> 4) : 0; // virtual blocks in the last window
+    // steps: the wave walks the maximum over its frames
+    uint32_t nst = (nw + G - 1 - q) / G; // this lane's windows
+    uint32_t mx = nst;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(mx, d);
+        mx = o > mx ? o : mx;
+    }
+    const uint32_t steps = __builtin_amdgcn_readfirstlane(mx);
+
+    const uint32_t vin = (uint32_t) A & 3u;
+    fe5 P1, P2, P3, P4, PG; // r^1..r^4, r^(4G)
+    uint32_t spad[4] = {0, 0, 0, 0}, wtag[4] = {0, 0, 0, 0}, fl = 0;
+    uint64_t H[5] = {0, 0, 0, 0, 0};
+    uint32_t tot[5] = {0, 0, 0, 0, 0}; // this lane's share of h
+    bool hasH = false;
+    uint32_t lastH = 0; // window index of the lane's last window below L
+    uint32_t ycarry = 0; // word 15 of window (this lane's window - 1), for q == 0
+    uint32_t dn[17];
+    if (nst > 0 && !(q == 0 && !DEC)) // encode's window 0 reads the payload itself
+        frame_load_raw(A, q, S, dn);
+
+#pragma unroll 1
+    for (uint32_t t = 0; t < steps; ++t) {
+        const uint32_t w = t * G + q;
+        const bool act = w < nw;
+        uint32_t dc[17];
+#pragma unroll
+        for (int k = 0; k < 17; ++k)
+            dc[k] = dn[k];
+        if (w + G < nw)
+            frame_load_raw(A, w + G, S, dn);
+        uint32_t x[16];
+        if (!DEC && w == 0) {
+            // plaintext bytes 0..31 = header || payload[0 .. 32-hl)
+            uint32_t pw16[16];
+            load_window(src, L_in < 32u ? (int) L_in : 32, pw16);
+            uint32_t pt[8];
+            switch (hl) {
+            case 1: shift_in<1>(pw16, pt); break;
+            case 2: shift_in<2>(pw16, pt); break;
+            case 8: shift_in<8>(pw16, pt); break;
+            default: shift_in<11>(pw16, pt); break;
+            }
+            pt[0] |= hw[0];
+            pt[1] |= hw[1];
+            pt[2] |= hw[2];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x[k] = 0;
+                x[8 + k] = pt[k];
+            }
+            if (S < 64u)
+                mask_tail(x, (int) S);
+        } else {
+            frame_words(dc, vin, w, S, x);
+        }
+        uint32_t ks[16];
+        salsa20_block(ks, key, n0, n1, w, 0);
+        // r from keystream block 0 (lane 0 of the group) to the group
+        if (t == 0) {
+            const fe r0 = poly_r_from_key(ks[0], ks[1], ks[2], ks[3]);
+            fe r;
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                r.l[k] = (uint32_t) __shfl((int) r0.l[k], (int) gbase);
+            P1 = fe5_of(r);
+            fe t2 = r;
+            fe_mul(t2, r);
+            P2 = fe5_of(t2);
+            fe t3 = t2;
+            fe_mul(t3, r);
+            P3 = fe5_of(t3);
+            fe t4 = t2;
+            fe_mul(t4, t2);
+            P4 = fe5_of(t4);
+            fe tg = t4;
+#pragma unroll
+            for (int k = 1; k < G; k <<= 1)
+                fe_mul(tg, tg); // r^(4G) by squaring (G = 1, 2, 4)
+            PG = fe5_of(tg);
+            if (w == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    spad[k] = ks[4 + k];
+            }
+        }
+        // ciphertext words c (the Poly1305 input) and output words y
+        uint32_t c[16], y[16];
+        if (DEC) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                c[k] = x[k];
+                y[k] = x[k] ^ ks[k];
+            }
+            if (S < 64u * w + 64u)
+                mask_tail(y, (int) (S - 64u * w));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                y[k] = c[k] = x[k] ^ ks[k];
+            if (S < 64u * w + 64u) {
+                mask_tail(c, (int) (S - 64u * w));
+                mask_tail(y, (int) (S - 64u * w));
+            }
+        }
+        if (w == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                c[k] = 0; // key area: not ciphertext
+        }
+        if (act) {
+            // Poly1305 contribution of this window
+            if (w < L) {
+                uint64_t a[5];
+                if (hasH) {
+#pragma unroll
+                    for (int k = 0; k < 5; ++k)
+                        a[k] = 0;
+                    uint32_t hh[5];
+                    const fe hf = fe_from_wide(H);
+#pragma unroll
+                    for (int k = 0; k < 5; ++k)
+                        hh[k] = hf.l[k];
+                    acc_mul(a, hh, PG);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 5; ++k)
+                        a[k] = 0;
+                }
+                uint32_t m[5];
+                if (w > 0) {
+                    block_limbs(c, 16, m);
+                    acc_mul(a, m, P4);
+                    block_limbs(c + 4, 16, m);
+                    acc_mul(a, m, P3);
+                }
+                block_limbs(c + 8, 16, m);
+                acc_mul(a, m, P2);
+                block_limbs(c + 12, 16, m);
+                acc_mul(a, m, P1);
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    H[k] = a[k];
+                hasH = true;
+                lastH = w;
+            } else {
+                // w == L: U'_L = sum_{j<kb} m_j r^(kb-j); window 0's j < 2 are zero
+                uint64_t a[5] = {0, 0, 0, 0, 0};
+                const int rem = (int) (S - 64u * w); // stream bytes in this window
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (j < (int) kb && !(w == 0 && j < 2)) {
+                        uint32_t m[5];
+                        const int nb = rem - 16 * j >= 16 ? 16 : rem - 16 * j;
+                        block_limbs(c + 4 * j, nb, m);
+                        const int e = (int) kb - j; // 1..4
+                        const fe5 pe = e == 1 ? P1 : e == 2 ? P2 : e == 3 ? P3 : P4;
+                        acc_mul(a, m, pe);
+                    }
+                }
+                const fe u = fe_from_wide(a);
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    tot[k] += u.l[k];
+            }
+        }
+        // window 0's extra outputs and state
+        if (w == 0 && act) {
+            if (DEC) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    wtag[k] = x[4 + k];
+                fl = y[8] & 3u;
+                // payload bytes 0 .. min(31, S-33) = plaintext bytes 1..
+                uint32_t pay[16];
+#pragma unroll
+                for (int k = 0; k < 7; ++k)
+                    pay[k] = __builtin_amdgcn_alignbyte(y[9 + k], y[8 + k], 1);
+                pay[7] = __builtin_amdgcn_alignbyte(0u, y[15], 1);
+#pragma unroll
+                for (int k = 8; k < 16; ++k)
+                    pay[k] = 0;
+                const int np = (int) (S < 64u ? S : 64u) - 33;
+                store_window(dst, np, pay);
+            } else {
+                uint32_t o[16];
+                o[0] = 0x53454d07u; // "\x07MESSAGE" || nonce
+                o[1] = 0x45474153u;
+                o[2] = n0;
+                o[3] = n1;
+#pragma unroll
+                for (int k = 4; k < 16; ++k)
+                    o[k] = 0;
+                store_window(dst, 16, o);
+                const int nc = (int) (S < 64u ? S : 64u) - 32;
+                uint32_t ct[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    ct[k] = k < 8 ? y[8 + k] : 0u;
+                store_window(dst + 32, nc, ct);
+            }
+        }
+        // the previous window's last output word: lane q-1 of this step, or
+        // (q == 0) lane G-1 of the previous step
+        const uint32_t y15 = act ? y[15] : 0u;
+        const uint32_t fromleft = (uint32_t) __shfl((int) y15, (int) (lane > 0 ? lane - 1 : 0));
+        const uint32_t yprev = q == 0 ? ycarry : fromleft;
+        if (act && w > 0)
+            frame_store(B, w, S, y, yprev, w == L);
+        ycarry = (uint32_t) __shfl((int) y15, (int) (gbase + G - 1));
+    }
+    // H_q * r^(kb + 4(L-1-lastH)), plus U'_L (already in tot)
+    if (hasH) {
+        fe e;
+        const uint32_t m4 = L - 1 - lastH; // 0 .. G-1
+        const fe5 pk = kb == 1 ? P1 : kb == 2 ? P2 : kb == 3 ? P3 : P4;
+        fe hf = fe_from_wide(H);
+        fe_mul_s(hf, pk.e, pk.s1, pk.s2, pk.s3, pk.s4);
+        e = hf;
+        for (uint32_t k = 0; k < m4; ++k) // at most G-1 times
+            fe_mul_s(e, P4.e, P4.s1, P4.s2, P4.s3, P4.s4);
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            tot[k] += e.l[k];
+    }
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1)
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            tot[k] += (uint32_t) __shfl_xor((int) tot[k], d);
+    if (is_big && q == 0) {
+        if (lb)
+            rp.excl[i] = excl;
+        big(i);
+    }
+    if (!valid || q != 0 || !small)
+        return;
+    if (S == 0) { // decode: header failure
+        status_out[i] = status;
+        flags_out[i] = 0;
+        if (L_in >= 33u) { // zero-filled payload region
+            for (uint32_t b = 0; b < L_in - 33u; ++b)
+                dst[b] = 0;
+        }
+        return;
+    }
+    uint64_t wide[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        wide[k] = tot[k];
+    uint32_t tag[4];
+    poly_finish(fe_from_wide(wide), spad, tag);
+    if (!DEC) {
+        uint32_t o[16] = {tag[0], tag[1], tag[2], tag[3]};
+        store_window(dst + 16, 16, o);
+    } else {
+        if (lb && !(vn > excl))
+            status = ZMQG_ERR_INVALID_SEQUENCE; // src/curve_mechanism_base.cpp:99-104 (before the MAC)
+        else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
+            status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
+        status_out[i] = status;
+        flags_out[i] = status == 0 ? (uint8_t) fl : 0;
+        if (status != 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the group's plaintext stores first
+            for (uint32_t b = 0; b < S - 33u; ++b)
+                dst[b] = 0;
+        }
+    }
+}
+
+} // namespace zmqg

@@ -7,20 +7,28 @@
 // The C ABI is include/zmqg_curve.h.
 //
 // Work decomposition:
-//   head kernel   one lane per frame: header checks, keystream block 0
-//                 (Poly1305 key r,s + first 32 ciphertext bytes), the powers
-//                 of r the body needs, and the frame's body chunk count.
-//   chunk scan    inclusive prefix sum of chunk counts (hipCUB).
-//   replay scan   decode only: per-session exclusive prefix max of accepted
-//                 nonces in batch order (hipCUB), = the reference's
-//                 sequential _cn_peer_nonce rule.
-//   body kernel   one lane per chunk = 2 Salsa20 blocks = 128 ciphertext
-//                 bytes = 8 Poly1305 blocks; lanes of a frame are adjacent,
-//                 so the per-chunk Poly1305 partials (each multiplied by its
-//                 power of r) are summed by a segmented wave reduction and
-//                 the segment leader finishes the tag; frames spanning
-//                 several waves combine through 64-bit atomics and an
-//                 arrival counter (last arriver finishes).
+//   frame kernel  G lanes per frame (curve_frames.hpp): every frame whose
+//                 stream fits kMaxFrameStream bytes is encoded/decoded whole
+//                 (keystream, Poly1305, tag) in one pass.  Decode also
+//                 records each frame's header-valid nonce for the replay rule.
+//   head kernel   one lane per larger frame: keystream block 0 (Poly1305
+//                 key r,s + first 32 ciphertext bytes), the powers of r the
+//                 body needs, and the frame's body chunks; the frame is
+//                 appended to the big-frame list (one packed atomic gives
+//                 its list position and chunk range together).
+//   body kernel   big frames: one lane per chunk = 2 Salsa20 blocks = 128
+//                 ciphertext bytes = 8 Poly1305 blocks; lanes of a frame are
+//                 adjacent, so the per-chunk Poly1305 partials (each
+//                 multiplied by its power of r) are summed by a segmented
+//                 wave reduction and the segment leader finishes the tag;
+//                 frames spanning several waves combine through 64-bit
+//                 atomics and an arrival counter (last arriver finishes).
+//   replay fixup  decode only: the reference's sequential _cn_peer_nonce
+//                 rule (src/curve_mechanism_base.cpp:98-106) in batch order
+//                 -- per-session exclusive prefix max of header-valid nonces
+//                 (one session: workgroup maxima + in-tile scan; several:
+//                 hipCUB sort-by-session + segmented scan) -- sets
+//                 INVALID_SEQUENCE and each session's new peer nonce.
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -33,6 +41,7 @@
 
 #include "../../include/zmqg_curve.h"
 #include "curve_device.hpp"
+#include "curve_frames.hpp"
 
 #ifndef ZMQG_ABLATE
 #define ZMQG_ABLATE 0
@@ -64,13 +73,8 @@ constexpr int kMaxPow = 25;           // r^(8*2^k), k < 25: frames up to 2^32 by
 constexpr uint32_t kIdle = 0xffffffffu;
 constexpr int kBodyThreads = 256; // 4 waves x 2 tile buffers of 9 KiB: 2 workgroups (8 waves) per CU
 constexpr int kHeadThreads = 256;
-
-struct DevSession {
-    uint32_t enc_key[8]; // HSalsa20(precom, enc_prefix)
-    uint32_t dec_key[8]; // HSalsa20(precom, dec_prefix)
-    uint32_t downgrade_sub;
-    uint32_t pad[7];
-};
+constexpr uint32_t kMaxFrameStream = 64 * 72; // frames up to 4.5 KiB of stream: frame kernel
+constexpr int kFixupThreads = 256;
 
 // Per-frame records written by the head kernel and read by the body kernel,
 // grouped by when a body lane needs them so each group is one batch of
@@ -102,7 +106,8 @@ struct __attribute__((aligned(16))) FrameFin { // tag / status inputs (64 B)
     uint32_t s[4];      // Poly1305 pad
     uint32_t tag[4];    // decode: tag carried on the wire
     uint32_t wire_len;  // decode: frame bytes on the wire
-    uint64_t peer_snap; // decode: session peer nonce before this batch
+    uint32_t frame;     // the frame's index in the batch
+    uint32_t pad;
 };
 static_assert(sizeof(FrameFin) == 64, "FrameFin layout");
 
@@ -124,6 +129,14 @@ struct Workspace {
     uint32_t *perm = nullptr;     // [cap]
     uint32_t *keys_s = nullptr;   // [cap]
     uint8_t *last = nullptr;      // [cap] last frame of its session in the batch
+    uint32_t *list_frame = nullptr;      // [cap] big-frame list: frame index at each position
+    unsigned long long *psnap = nullptr; // [cap] session peer nonce before the batch, per frame
+    unsigned long long *blockmax = nullptr; // [cap] frame-kernel workgroup maxima of vout
+    unsigned long long *list_ctr = nullptr; // [2] big frames << 40 | body chunks, by call parity
+    uint32_t *ticket = nullptr;             // [2] frame-kernel workgroup tickets, by call parity
+    unsigned long long *lb_flag = nullptr;  // [cap] look-back state per workgroup ticket
+    unsigned long long *lb_agg = nullptr;   // [cap]
+    unsigned long long *lb_inc = nullptr;   // [cap]
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };
@@ -147,7 +160,8 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[4];
+    uint32_t calls = 0; // batch calls so far: list/ticket parity, look-back epoch
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
     char last_error[256] = {0};
     std::mutex mu;
@@ -241,46 +255,6 @@ __device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, FramePow 
     }
 }
 
-// plaintext header of src/curve_mechanism_base.cpp:118-158 as 3 words
-__device__ __forceinline__ uint32_t plaintext_header(uint32_t msg_flags, uint32_t downgrade, uint32_t hw[3])
-{
-    const uint32_t f = msg_flags & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND);
-    const uint32_t ct = msg_flags & 0x1c;
-    const bool sub = ct == ZMQG_MSG_SUBSCRIBE, cancel = ct == ZMQG_MSG_CANCEL;
-    hw[1] = hw[2] = 0;
-    if (!(sub || cancel)) {
-        hw[0] = f;
-        return 1;
-    }
-    if (downgrade) {
-        hw[0] = f | ((sub ? 1u : 0u) << 8);
-        return 2;
-    }
-    if (cancel) { // f|2, "\x06CANCEL"
-        hw[0] = (f | 2u) | (6u << 8) | ((uint32_t) 'C' << 16) | ((uint32_t) 'A' << 24);
-        hw[1] = (uint32_t) 'N' | ((uint32_t) 'C' << 8) | ((uint32_t) 'E' << 16) | ((uint32_t) 'L' << 24);
-        return 8;
-    }
-    // f|2, "\x09SUBSCRIBE"
-    hw[0] = (f | 2u) | (9u << 8) | ((uint32_t) 'S' << 16) | ((uint32_t) 'U' << 24);
-    hw[1] = (uint32_t) 'B' | ((uint32_t) 'S' << 8) | ((uint32_t) 'C' << 16) | ((uint32_t) 'R' << 24);
-    hw[2] = (uint32_t) 'I' | ((uint32_t) 'B' << 8) | ((uint32_t) 'E' << 16);
-    return 11;
-}
-
-// out[i] = stream bytes of p shifted right by HL bytes (zeros shifted in), 8 words.
-template <int HL>
-__device__ __forceinline__ void shift_in(const uint32_t p[16], uint32_t out[8])
-{
-    constexpr int A = HL >> 2, B = HL & 3;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t hi = (i - A >= 0) ? p[i - A] : 0u;
-        const uint32_t lo = (i - A - 1 >= 0) ? p[i - A - 1] : 0u;
-        out[i] = B == 0 ? hi : __builtin_amdgcn_alignbyte(hi, lo, 4 - B);
-    }
-}
-
 // =====================================================================
 // session setup
 // =====================================================================
@@ -311,29 +285,73 @@ __global__ void k_set_peer(unsigned long long *peer, uint32_t sid, unsigned long
 // =====================================================================
 // encode
 // =====================================================================
-__global__ __launch_bounds__(kHeadThreads) void k_encode_head(
-    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce,
-    const uint8_t *__restrict__ flags, const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len,
-    const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
-    const DevSession *__restrict__ sessions, uint32_t max_sessions, FrameHot *__restrict__ hot,
-    FramePow *__restrict__ pw, FrameFin *__restrict__ fin, uint32_t *__restrict__ powtab,
-    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, uint32_t *__restrict__ nch_out)
+// Big-frame list: one packed atomic gives a frame its list position (high
+// 24 bits) and its body chunk range (low 40 bits) together, so chunk_end is
+// increasing in list position whatever order the frames arrive in.
+__device__ __forceinline__ uint32_t list_append(unsigned long long *list_ctr, uint32_t *chunk_end,
+                                                uint32_t *list_frame, uint32_t i, uint32_t nch)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
+    const unsigned long long old = atomicAdd(list_ctr, (1ull << 40) | nch);
+    const uint32_t pos = (uint32_t) (old >> 40);
+    chunk_end[pos] = (uint32_t) (old & ((1ull << 40) - 1)) + nch;
+    list_frame[pos] = i;
+    return pos;
+}
+
+// Where the chunked path keeps a big frame's records (indexed by list position).
+struct BigRecords {
+    FrameHot *hot;
+    FramePow *pw;
+    FrameFin *fin;
+    uint32_t *powtab;
+    unsigned long long *acc;
+    uint32_t *cnt;
+    unsigned long long *list_ctr; // this call's big-frame list counter
+    uint32_t *chunk_end;
+    uint32_t *list_frame;
+};
+
+// The chunked path's head for one encode frame whose stream exceeds the
+// frame kernel's limit (called by the frame kernel on one lane): keystream
+// block 0, records for the body, list entry.
+struct EncodeHead {
+    const uint32_t *sid;
+    const uint64_t *nonce;
+    const uint8_t *flags;
+    const uint64_t *in_off;
+    const uint32_t *len;
+    const uint8_t *in;
+    const uint64_t *out_off;
+    uint8_t *out;
+    const DevSession *sessions;
+    uint32_t max_sessions;
+    BigRecords R;
+    __device__ void operator()(uint32_t i) const;
+};
+
+__device__ void EncodeHead::operator()(uint32_t i) const
+{
+    FrameHot *hot = R.hot;
+    FramePow *pw = R.pw;
+    FrameFin *fin = R.fin;
+    uint32_t *powtab = R.powtab;
+    unsigned long long *acc = R.acc;
+    uint32_t *cnt = R.cnt;
     const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
     const DevSession &ses = sessions[s];
+    const uint32_t P = len[i];
+    uint32_t hw[3];
+    const uint32_t hl = plaintext_header(flags[i], ses.downgrade_sub, hw);
+    const uint32_t mlen = hl + P;
+    uint32_t nch, blast;
+    body_geometry(mlen, nch, blast);
+    const uint32_t p = list_append(R.list_ctr, R.chunk_end, R.list_frame, i, nch);
     FrameHot H;
 #pragma unroll
     for (int t = 0; t < 8; ++t)
         H.key[t] = ses.enc_key[t];
     const uint64_t nc = nonce[i];
     const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
-    const uint32_t P = len[i];
-    uint32_t hw[3];
-    const uint32_t hl = plaintext_header(flags[i], ses.downgrade_sub, hw);
-    const uint32_t mlen = hl + P;
 
     uint32_t ks[16];
     salsa20_block(ks, H.key, n0, n1, 0, 0);
@@ -371,10 +389,8 @@ __global__ __launch_bounds__(kHeadThreads) void k_encode_head(
     const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
     poly_absorb64(h, r, s1, s2, s3, s4, ct, nv0);
 
-    uint32_t nch, blast;
-    body_geometry(mlen, nch, blast);
     fe hf;
-    head_powers(r, nch, blast, pw + i, powtab + (size_t) i * kMaxPow * 5, hf);
+    head_powers(r, nch, blast, pw + p, powtab + (size_t) p * kMaxPow * 5, hf);
     if (mlen > 32)
         fe_mul(h, hf);
 
@@ -388,7 +404,7 @@ __global__ __launch_bounds__(kHeadThreads) void k_encode_head(
     H.flags = 0;
     H.in_base = (uint64_t) (uintptr_t) src;
     H.out_base = (uint64_t) (uintptr_t) o;
-    hot[i] = H;
+    hot[p] = H;
     FrameFin F;
     store_fe(F.hh, h);
 #pragma unroll
@@ -397,13 +413,13 @@ __global__ __launch_bounds__(kHeadThreads) void k_encode_head(
         F.tag[t] = 0;
     }
     F.wire_len = mlen + 32;
-    F.peer_snap = 0;
-    fin[i] = F;
+    F.frame = i;
+    F.pad = 0;
+    fin[p] = F;
 #pragma unroll
     for (int t = 0; t < 5; ++t)
-        acc[(size_t) i * 5 + t] = 0;
-    cnt[i] = 0;
-    nch_out[i] = nch;
+        acc[(size_t) p * 5 + t] = 0;
+    cnt[p] = 0;
 }
 
 // Segmented (by frame) sum of the lanes' Poly1305 contributions over one
@@ -454,81 +470,60 @@ __device__ __forceinline__ bool frame_combine(uint32_t g0, uint32_t nch, unsigne
 // =====================================================================
 // decode
 // =====================================================================
-__global__ __launch_bounds__(kHeadThreads) void k_decode_head(
-    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ in_off,
-    const uint32_t *__restrict__ wire_len, const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off,
-    uint8_t *__restrict__ out, const DevSession *__restrict__ sessions, uint32_t max_sessions,
-    const unsigned long long *__restrict__ peer, FrameHot *__restrict__ hot, FramePow *__restrict__ pw,
-    FrameFin *__restrict__ fin, uint32_t *__restrict__ powtab, unsigned long long *__restrict__ acc,
-    uint32_t *__restrict__ cnt, uint32_t *__restrict__ nch_out, unsigned long long *__restrict__ vout,
-    uint32_t *__restrict__ iota, uint8_t *__restrict__ last_single)
+// The chunked path's head for one decode frame with a valid header whose
+// stream exceeds the frame kernel's limit (called by the frame kernel on one
+// lane; header failures never get here).
+struct DecodeHead {
+    const uint32_t *sid;
+    const uint64_t *in_off;
+    const uint32_t *wire_len;
+    const uint8_t *in;
+    const uint64_t *out_off;
+    uint8_t *out;
+    const DevSession *sessions;
+    uint32_t max_sessions;
+    BigRecords R;
+    __device__ void operator()(uint32_t i) const;
+};
+
+__device__ void DecodeHead::operator()(uint32_t i) const
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
+    FrameHot *hot = R.hot;
+    FramePow *pw = R.pw;
+    FrameFin *fin = R.fin;
+    uint32_t *powtab = R.powtab;
+    unsigned long long *acc = R.acc;
+    uint32_t *cnt = R.cnt;
     const uint32_t wl = wire_len[i];
+    const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
     const uint8_t *src = in + in_off[i];
     uint8_t *dst = out + out_off[i];
     uint32_t w[16];
-    load_window(src, wl < 64 ? (int) wl : 64, w);
-    const uint32_t b0 = w[0] & 0xff;
-    int32_t status = 0;
-    if (wl <= 1 || wl <= b0)
-        status = ZMQG_ERR_MALFORMED_UNSPECIFIED; // src/mechanism_base.cpp:16-22
-    else if (wl < 8 || w[0] != 0x53454d07u || w[1] != 0x45474153u)
-        status = ZMQG_ERR_UNEXPECTED_COMMAND; // src/curve_mechanism_base.cpp:85-90
-    else if (wl < 33)
-        status = ZMQG_ERR_MALFORMED_MESSAGE; // :92-96
-
+    load_window(src, 64, w); // wl > kMaxFrameStream >= 64
+    const uint32_t mlen = wl - 32;
+    uint32_t nch, blast;
+    body_geometry(mlen, nch, blast);
+    const uint32_t p = list_append(R.list_ctr, R.chunk_end, R.list_frame, i, nch);
 #pragma unroll
     for (int t = 0; t < 5; ++t)
-        acc[(size_t) i * 5 + t] = 0;
-    cnt[i] = 0;
-    iota[i] = i;
-    if (last_single)
-        last_single[i] = (i + 1 == n) ? 1 : 0;
+        acc[(size_t) p * 5 + t] = 0;
+    cnt[p] = 0;
 
     FrameHot H;
     FrameFin F;
     F.wire_len = wl;
-    F.peer_snap = peer[s];
-    H.status = status;
+    F.frame = i;
+    F.pad = 0;
+    H.status = 0;
     H.hl = 0;
     H.in_base = (uint64_t) (uintptr_t) src;
     H.out_base = (uint64_t) (uintptr_t) dst;
-    if (status != 0) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-            H.key[t] = 0;
-        store_fe(H.r, fe_zero());
-        H.nch = 1;
-        H.mlen = 0;
-        H.n0 = H.n1 = 0;
-        H.flags = 0;
-        store_fe(pw[i].rb, fe_zero());
-#pragma unroll
-        for (int k = 0; k < kPowInline; ++k)
-            store_fe(pw[i].t[k], fe_zero());
-        store_fe(F.hh, fe_zero());
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            F.s[t] = F.tag[t] = 0;
-        hot[i] = H;
-        fin[i] = F;
-        nch_out[i] = 1;
-        vout[i] = 0;
-        return;
-    }
-    const uint64_t nc = ((uint64_t) bswap32(w[2]) << 32) | bswap32(w[3]);
-    const uint32_t mlen = wl - 32;
 #pragma unroll
     for (int t = 0; t < 8; ++t)
         H.key[t] = sessions[s].dec_key[t];
     uint32_t ks[16];
     salsa20_block(ks, H.key, w[2], w[3], 0, 0);
     const fe r = poly_r_from_key(ks[0], ks[1], ks[2], ks[3]);
-    const int nv0 = mlen < 32 ? (int) mlen : 32;
     uint32_t ct[16];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -537,29 +532,25 @@ __global__ __launch_bounds__(kHeadThreads) void k_decode_head(
     }
     fe h = fe_zero();
     const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
-    poly_absorb64(h, r, s1, s2, s3, s4, ct, nv0);
+    poly_absorb64(h, r, s1, s2, s3, s4, ct, 32);
     uint32_t pt[16];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         pt[t] = ct[t] ^ ks[8 + t];
         pt[8 + t] = 0;
     }
-    mask_tail(pt, nv0);
-    // payload bytes 0 .. nv0-2 = plaintext bytes 1 .. nv0-1 (speculative:
-    // zeroed by the finisher if the frame fails)
+    // payload bytes 0 .. 30 = plaintext bytes 1 .. 31 (speculative: zeroed
+    // by the finisher or the replay fixup if the frame fails)
     uint32_t pay[16];
 #pragma unroll
     for (int t = 0; t < 15; ++t)
         pay[t] = __builtin_amdgcn_alignbyte(pt[t + 1], pt[t], 1);
     pay[15] = 0;
-    store_window(dst, nv0 - 1, pay);
+    store_window(dst, 31, pay);
 
-    uint32_t nch, blast;
-    body_geometry(mlen, nch, blast);
     fe hf;
-    head_powers(r, nch, blast, pw + i, powtab + (size_t) i * kMaxPow * 5, hf);
-    if (mlen > 32)
-        fe_mul(h, hf);
+    head_powers(r, nch, blast, pw + p, powtab + (size_t) p * kMaxPow * 5, hf);
+    fe_mul(h, hf);
     store_fe(H.r, r);
     H.nch = nch;
     H.mlen = mlen;
@@ -572,10 +563,8 @@ __global__ __launch_bounds__(kHeadThreads) void k_decode_head(
         F.s[t] = ks[4 + t];
         F.tag[t] = w[4 + t];
     }
-    hot[i] = H;
-    fin[i] = F;
-    nch_out[i] = nch;
-    vout[i] = nc;
+    hot[p] = H;
+    fin[p] = F;
 }
 
 __global__ void k_gather_u64(uint32_t n, const uint32_t *__restrict__ perm, const unsigned long long *__restrict__ src,
@@ -598,14 +587,46 @@ __global__ void k_scatter_replay(uint32_t n, const uint32_t *__restrict__ perm, 
     last[m] = (i + 1 == n || keys_s[i + 1] != keys_s[i]) ? 1 : 0;
 }
 
-
-// src/curve_mechanism_base.cpp:99-104: the wire nonce must exceed the peer
-// nonce, which (batch order) is the max of the session's prior value and
-// every earlier header-valid nonce of the session in this batch.
-__device__ __forceinline__ bool sequence_ok(uint64_t nonce, unsigned long long peer_snap, unsigned long long excl)
+// Replay rule of src/curve_mechanism_base.cpp:98-106 for a batch over
+// several sessions, as if the frames were decoded one by one in batch
+// order: a header-valid frame passes iff its nonce exceeds max(its session's
+// peer nonce before the batch, every earlier header-valid nonce of that
+// session in the batch) -- excl, from the sort-by-session path; the peer
+// nonce is set before the MAC check, so a MAC failure still advances it.
+// Small frames get INVALID_SEQUENCE, flags 0 and a zero-filled payload here
+// (big frames in the body finisher, which runs before); the last frame of
+// each session writes the session's new peer nonce = max(before, all its
+// header-valid nonces).  (One session: the frame kernel does all of this.)
+__global__ __launch_bounds__(kFixupThreads) void k_fixup(
+    uint32_t n, uint32_t max_stream, const unsigned long long *__restrict__ vout,
+    const unsigned long long *__restrict__ psnap, const unsigned long long *__restrict__ excl,
+    const uint8_t *__restrict__ last, const uint32_t *__restrict__ sid, uint32_t max_sessions,
+    const uint32_t *__restrict__ wire_len, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+    int32_t *__restrict__ status_out, uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ peer)
 {
-    const unsigned long long prev = excl > peer_snap ? excl : peer_snap;
-    return nonce > prev;
+    const uint32_t i = blockIdx.x * kFixupThreads + threadIdx.x;
+    if (i >= n)
+        return;
+    const unsigned long long v = vout[i], ex = excl[i], ps = psnap[i];
+    const unsigned long long prev = ex > ps ? ex : ps;
+    const uint32_t wl = wire_len[i];
+    const int32_t st = status_out[i];
+    const bool header_ok = st == 0 || st == ZMQG_ERR_CRYPTOGRAPHIC || st == ZMQG_ERR_INVALID_SEQUENCE;
+    if (header_ok && wl <= max_stream && !(v > prev) && st != ZMQG_ERR_INVALID_SEQUENCE) {
+        status_out[i] = ZMQG_ERR_INVALID_SEQUENCE;
+        flags_out[i] = 0;
+        if (st == 0) { // (a MAC failure is already zero-filled)
+            uint8_t *o = out + out_off[i];
+            for (uint32_t b = 0; b + 33 < wl; ++b)
+                o[b] = 0;
+        }
+    }
+    if (last[i]) {
+        unsigned long long pn = prev;
+        if (header_ok && v > pn)
+            pn = v;
+        peer[sid[i] < max_sessions ? sid[i] : 0] = pn;
+    }
 }
 
 // ---------------------------------------------------------------- body
@@ -683,18 +704,14 @@ __device__ __forceinline__ uint32_t byte_mask_below(int e, int k) // bytes [4k, 
 struct TileRecords {
     u32x4 h[6]; // FrameHot
     u32x4 p[7]; // FramePow
-    unsigned long long ex; // decode: replay-scan exclusive max
-    unsigned long long psnap; // decode: session peer nonce before the batch
 };
 static_assert(sizeof(FrameHot) == 6 * 16 && sizeof(FramePow) == 7 * 16, "records");
 
 // Unconditional loads (an idle lane reads frame 0's records and ignores
 // them): a conditional load would need a register copy at the branch join,
 // and that copy waits for the load.
-template <bool DEC>
 __device__ __forceinline__ void load_records(TileRecords &R, uint32_t i, const FrameHot *__restrict__ hot,
-                                             const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
-                                             const unsigned long long *__restrict__ excl)
+                                             const FramePow *__restrict__ pw)
 {
     const GCU4 *ph = (const GCU4 *) (hot + i), *pp = (const GCU4 *) (pw + i);
 #pragma unroll
@@ -703,13 +720,6 @@ __device__ __forceinline__ void load_records(TileRecords &R, uint32_t i, const F
 #pragma unroll
     for (int q = 0; q < 7; ++q)
         R.p[q] = pp[q];
-    if (DEC) {
-        R.ex = excl[i];
-        R.psnap = fin[i].peer_snap;
-    } else {
-        R.ex = 0;
-        R.psnap = 0;
-    }
 }
 
 template <int W>
@@ -762,7 +772,6 @@ __device__ __forceinline__ uint64_t tile_setup(TileLane &T, const TileRecords &R
 #pragma unroll
     for (int q = 0; q < 7; ++q)
         asm volatile("" ::"v"(R.p[q]));
-    asm volatile("" ::"v"(R.ex), "v"(R.psnap));
     // FrameHot words: key 0-7, r 8-12, nch 13, mlen 14, hl 15, n0 16, n1 17,
     // status 18, flags 19, in_base 20-21, out_base 22-23
     T.k[0] = rec_word<0>(R.h);
@@ -803,8 +812,7 @@ __device__ __forceinline__ uint64_t tile_setup(TileLane &T, const TileRecords &R
         const uint32_t P0 = 32 + kChunk * T.c; // first plaintext byte of this chunk
         uint32_t L = mlen > P0 ? (mlen - P0 < kChunk ? mlen - P0 : kChunk) : 0;
         if (DEC) {
-            const uint64_t nc = ((uint64_t) bswap32(T.n0) << 32) | bswap32(T.n1);
-            if (T.status != 0 || !sequence_ok(nc, R.psnap, R.ex))
+            if (T.status != 0)
                 L = 0;
             src = in_base + 32 + P0;     // ciphertext byte P0 on the wire
             T.dst = T.out_base + P0 - 1; // plaintext byte P0 = payload byte P0-1
@@ -912,18 +920,23 @@ __device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t
     }
 }
 
+// The big-frame list (positions 0 .. n-1, written by the head kernel) is
+// read from *list_ctr: n = entries, total = body chunks.
 template <bool DEC>
 __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_body(
-    uint32_t n, const uint32_t *__restrict__ chunk_end, const FrameHot *__restrict__ hot,
-    const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin, const uint32_t *__restrict__ powtab,
-    uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out, const uint32_t *__restrict__ sid,
-    uint32_t max_sessions, unsigned long long *__restrict__ peer, unsigned long long *__restrict__ acc,
-    uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl, const uint8_t *__restrict__ last)
+    const unsigned long long *__restrict__ list_ctr, const uint32_t *__restrict__ chunk_end,
+    const FrameHot *__restrict__ hot, const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
+    const uint32_t *__restrict__ powtab, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
+    unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
+    const unsigned long long *__restrict__ psnap)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kBufLds];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t *const wlds = lds + wv * 2 * kBufLds;
-    const uint32_t total = chunk_end[n - 1];
+    const unsigned long long lc = *list_ctr;
+    const uint32_t n = (uint32_t) (lc >> 40), total = (uint32_t) (lc & ((1ull << 40) - 1));
+    if (n == 0)
+        return;
     const uint64_t tiles = (total + 63) >> 6;
     const uint64_t W = (uint64_t) blockIdx.x * kBodyWaves + wv, NW = (uint64_t) gridDim.x * kBodyWaves;
     const uint32_t tb = (uint32_t) (tiles * W / NW), te = (uint32_t) (tiles * (W + 1) / NW);
@@ -939,7 +952,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         const uint32_t g = 64 * tb + lane;
         const FrameLook lk = window_find(window_load(chunk_end, n, lo), lo, n, g);
         TileRecords R;
-        load_records<DEC>(R, g < total ? lk.i : 0, hot, pw, fin, excl);
+        load_records(R, g < total ? lk.i : 0, hot, pw);
         const uint64_t src = tile_setup<DEC>(cur, R, g < total, lk, g, powtab);
         tile_dma(wlds, src, cur.L);
         if (tb + 1 < te) {
@@ -963,26 +976,19 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         // ---- issue: next tile's records, the chunk-end window after it
         const uint32_t gn = 64 * (t + 1) + lane;
         TileRecords Rn;
-        load_records<DEC>(Rn, has_next && gn < total ? lkn.i : 0, hot, pw, fin, excl);
+        load_records(Rn, has_next && gn < total ? lkn.i : 0, hot, pw);
         // (unconditional: on the last two tiles this reads a clamped, unused window)
         const uint32_t lo2 = next_tile_lo(lkn, 64 * (t + 2));
         const uint32_t ce2 = window_load(chunk_end, n, lo2 < n ? lo2 : n - 1);
         // ---- issue: this tile's finish inputs (used after its stores, so that
         // waiting for them does not wait for the stores)
         u32x4 Fq[4];
-        uint32_t f_last = 0, f_sid = 0;
-        unsigned long long f_ex = 0;
         {
             const uint32_t fi = cur.key != kIdle ? cur.key : 0;
             const GCU4 *pf = (const GCU4 *) (fin + fi);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 Fq[q] = pf[q];
-            if (DEC) {
-                f_last = last[fi];
-                f_sid = sid[fi];
-                f_ex = excl[fi];
-            }
         }
         // ---- compute: keystream, MAC, output image (in place, one window behind)
         uint64_t v[5] = {0, 0, 0, 0, 0};
@@ -1106,55 +1112,38 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             asm volatile("" ::"v"(Fq[q])); // (see tile_setup: keep every loaded word's register)
-        asm volatile("" ::"v"(f_last), "v"(f_sid), "v"(f_ex));
         if (ZMQG_ABLATE != 4 && wave_segment_sum(cur.key, v)) {
-            const uint32_t i = cur.key;
-            if (frame_combine(cur.g0, cur.nch, acc + (size_t) i * 5, cnt + i, v)) {
-                // FrameFin words: hh 0-4, s 5-8, tag 9-12, wire_len 13, peer_snap 14-15
+            const uint32_t p = cur.key; // list position
+            if (frame_combine(cur.g0, cur.nch, acc + (size_t) p * 5, cnt + p, v)) {
+                // FrameFin words: hh 0-4, s 5-8, tag 9-12, wire_len 13, frame 14
                 const fe hh = rec_fe<0>(Fq);
                 const uint32_t fs[4] = {rec_word<5>(Fq), rec_word<6>(Fq), rec_word<7>(Fq), rec_word<8>(Fq)};
-                if (!DEC) {
 #pragma unroll
-                    for (int q = 0; q < 5; ++q)
-                        v[q] += hh.l[q];
+                for (int q = 0; q < 5; ++q)
+                    v[q] += hh.l[q];
+                if (!DEC) {
                     uint32_t tag[16];
                     poly_finish(fe_from_wide(v), fs, tag);
                     store_window((uint8_t *) (uintptr_t) cur.out_base + 16, 16, tag);
                 } else {
                     const uint32_t wtag[4] = {rec_word<9>(Fq), rec_word<10>(Fq), rec_word<11>(Fq), rec_word<12>(Fq)};
-                    const uint32_t wire_len = rec_word<13>(Fq);
-                    const unsigned long long psnap = ((uint64_t) rec_word<15>(Fq) << 32) | rec_word<14>(Fq);
-                    int32_t status = cur.status;
-                    const unsigned long long ex = f_ex;
-                    const uint64_t nc = ((uint64_t) bswap32(cur.n0) << 32) | bswap32(cur.n1);
-                    if (status == 0 && !sequence_ok(nc, psnap, ex))
-                        status = ZMQG_ERR_INVALID_SEQUENCE;
-                    if (status == 0) {
-#pragma unroll
-                        for (int q = 0; q < 5; ++q)
-                            v[q] += hh.l[q];
-                        uint32_t tag[4];
-                        poly_finish(fe_from_wide(v), fs, tag);
-                        const uint32_t diff =
-                            (tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]);
-                        if (diff)
-                            status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
-                    }
+                    const uint32_t wire_len = rec_word<13>(Fq), i = rec_word<14>(Fq);
+                    // replay rule first (src/curve_mechanism_base.cpp:99-104), then the MAC
+                    const unsigned long long nc = ((uint64_t) bswap32(cur.n0) << 32) | bswap32(cur.n1);
+                    const unsigned long long ex = excl[i], ps = psnap[i];
+                    uint32_t tag[4];
+                    poly_finish(fe_from_wide(v), fs, tag);
+                    const uint32_t diff =
+                        (tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]);
+                    const int32_t status = !(nc > ex && nc > ps) ? ZMQG_ERR_INVALID_SEQUENCE
+                                           : diff              ? ZMQG_ERR_CRYPTOGRAPHIC // :277-281
+                                                               : 0;
                     status_out[i] = status;
                     flags_out[i] = status == 0 ? (uint8_t) cur.flags : 0;
-                    if (status != 0 && wire_len >= 33) {
+                    if (status != 0) {
                         uint8_t *o = (uint8_t *) (uintptr_t) cur.out_base;
                         for (uint32_t b = 0; b < wire_len - 33; ++b)
                             o[b] = 0;
-                    }
-                    if (f_last) {
-                        // _cn_peer_nonce after the batch: max over accepted headers
-                        unsigned long long p = psnap;
-                        if (ex > p)
-                            p = ex;
-                        if (cur.status == 0 && nc > p)
-                            p = nc;
-                        peer[f_sid < max_sessions ? f_sid : 0] = p;
                     }
                 }
             }
@@ -1203,18 +1192,23 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
             (rc = grow(ctx, w.acc, cap * 5)) || (rc = grow(ctx, w.cnt, cap)) || (rc = grow(ctx, w.nch, cap)) ||
             (rc = grow(ctx, w.chunk_end, cap)) || (rc = grow(ctx, w.v, cap)) || (rc = grow(ctx, w.excl, cap)) ||
             (rc = grow(ctx, w.v_s, cap)) || (rc = grow(ctx, w.excl_s, cap)) || (rc = grow(ctx, w.iota, cap)) ||
-            (rc = grow(ctx, w.perm, cap)) || (rc = grow(ctx, w.keys_s, cap)) || (rc = grow(ctx, w.last, cap)))
+            (rc = grow(ctx, w.perm, cap)) || (rc = grow(ctx, w.keys_s, cap)) || (rc = grow(ctx, w.last, cap)) ||
+            (rc = grow(ctx, w.list_frame, cap)) || (rc = grow(ctx, w.psnap, cap)) ||
+            (rc = grow(ctx, w.blockmax, cap)) || (rc = grow(ctx, w.lb_flag, cap)) || (rc = grow(ctx, w.lb_agg, cap)) ||
+            (rc = grow(ctx, w.lb_inc, cap)))
             return rc;
+        ZCHECK(ctx, hipMemset(w.lb_flag, 0, cap * sizeof(unsigned long long)));
+        if (!w.list_ctr) {
+            if ((rc = grow(ctx, w.list_ctr, 2)) || (rc = grow(ctx, w.ticket, 2)))
+                return rc;
+            ZCHECK(ctx, hipMemset(w.list_ctr, 0, 2 * sizeof(unsigned long long)));
+            ZCHECK(ctx, hipMemset(w.ticket, 0, 2 * sizeof(uint32_t)));
+        }
         w.cap = cap;
     }
     // hipCUB temporaries for n frames
     size_t need = 0, b = 0;
     const int nn = (int) n;
-    ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, b, w.nch, w.chunk_end, nn));
-    need = b > need ? b : need;
-    b = 0;
-    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScan(nullptr, b, w.v, w.excl, hipcub::Max(), 0ull, nn));
-    need = b > need ? b : need;
     if (ctx->sort_bits > 0) {
         b = 0;
         ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t *) nullptr, w.keys_s,
@@ -1288,6 +1282,31 @@ struct ProfSpan {
     }
 };
 
+// Lanes per frame for the frame kernel: enough waves for >= 2 per SIMD.
+int lanes_per_frame(uint32_t n)
+{
+    return n >= 131072u ? 1 : n >= 32768u ? 2 : 4;
+}
+
+template <bool DEC, class BigOp>
+void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const uint64_t *nonce,
+                   const uint8_t *flags, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
+                   const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
+                   uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, unsigned long long *zero_next)
+{
+    const dim3 grid((uint32_t) (((uint64_t) n * G + 255) / 256));
+#define ZMQG_LAUNCH_FRAMES(GG)                                                                                        \
+    hipLaunchKernelGGL((k_frames<DEC, GG, BigOp>), grid, dim3(256), 0, st, n, sid, nonce, flags, in_off, len, in,      \
+                       out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zero_next)
+    if (G == 1)
+        ZMQG_LAUNCH_FRAMES(1);
+    else if (G == 2)
+        ZMQG_LAUNCH_FRAMES(2);
+    else
+        ZMQG_LAUNCH_FRAMES(4);
+#undef ZMQG_LAUNCH_FRAMES
+}
+
 } // namespace
 
 extern "C" {
@@ -1342,7 +1361,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     (void) hipDeviceSynchronize();
     Workspace &w = ctx->ws;
     void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
-                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
+                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.psnap, w.blockmax, w.list_ctr,
+                    w.ticket, w.lb_flag, w.lb_agg, w.lb_inc, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
             (void) hipFree(p);
@@ -1371,7 +1391,7 @@ int zmqg_ctx_set_profiling(zmqg_ctx *ctx, int enable)
 
 int zmqg_ctx_get_profile(zmqg_ctx *ctx, int kind, double *ms_total, uint64_t *launches)
 {
-    if (!ctx || kind < 0 || kind > 3 || !ms_total || !launches)
+    if (!ctx || kind < 0 || kind > 5 || !ms_total || !launches)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
     ZCHECK(ctx, hipDeviceSynchronize());
@@ -1496,17 +1516,22 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         return rc;
     Workspace &w = ctx->ws;
     const uint32_t nn = (uint32_t) n;
+    const int G = lanes_per_frame(nn);
+    const uint32_t par = ctx->calls++ & 1u;
+    const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.list_ctr + par, w.chunk_end, w.list_frame};
     ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
-    hipLaunchKernelGGL(k_encode_head, dim3((nn + kHeadThreads - 1) / kHeadThreads), dim3(kHeadThreads), 0, st, nn,
-                       sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions, ctx->max_sessions, w.hot,
-                       w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch);
+    ProfSpan main(ctx, ZMQG_PROF_ENCODE_MAIN, st);
+    launch_frames<false>(G, nn, st, sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
+                         ctx->max_sessions, nullptr, nullptr, ReplayOut{},
+                         EncodeHead{sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
+                                    ctx->max_sessions, R},
+                         w.list_ctr + (par ^ 1u));
     ZCHECK(ctx, hipGetLastError());
-    size_t tb = w.temp_bytes;
-    ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
+    main.end();
     ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
-    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
-                       w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, sid, ctx->max_sessions,
-                       ctx->peer, w.acc, w.cnt, (const unsigned long long *) nullptr, (const uint8_t *) nullptr);
+    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, R.list_ctr, w.chunk_end, w.hot,
+                       w.pw, w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, w.acc, w.cnt,
+                       (const unsigned long long *) nullptr, (const unsigned long long *) nullptr);
     ZCHECK(ctx, hipGetLastError());
     body.end();
     call.end();
@@ -1531,16 +1556,35 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     Workspace &w = ctx->ws;
     const uint32_t nn = (uint32_t) n;
     const dim3 hgrid((nn + kHeadThreads - 1) / kHeadThreads);
-    ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
-    hipLaunchKernelGGL(k_decode_head, hgrid, dim3(kHeadThreads), 0, st, nn, sid, in_off, wire_len, in, out_off, out,
-                       ctx->sessions, ctx->max_sessions, ctx->peer, w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch,
-                       w.v, w.iota, ctx->sort_bits == 0 ? w.last : (uint8_t *) nullptr);
-    ZCHECK(ctx, hipGetLastError());
-    size_t tb = w.temp_bytes;
-    if (ctx->sort_bits == 0) {
-        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScan(w.temp, tb, w.v, w.excl, hipcub::Max(), 0ull, (int) nn, st));
+    const int G = lanes_per_frame(nn);
+    const bool multi = ctx->sort_bits > 0;
+    const uint32_t par = ctx->calls++ & 1u, epoch = ctx->calls; // epoch >= 1
+    const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.list_ctr + par, w.chunk_end, w.list_frame};
+    ReplayOut rp{};
+    rp.vout = w.v;
+    rp.psnap = w.psnap;
+    rp.peer = ctx->peer;
+    if (multi) {
+        rp.iota = w.iota;
     } else {
-        tb = w.temp_bytes;
+        rp.excl = w.excl;
+        rp.ticket = w.ticket + par;
+        rp.ticket_next = w.ticket + (par ^ 1u);
+        rp.lb_flag = w.lb_flag;
+        rp.lb_agg = w.lb_agg;
+        rp.lb_inc = w.lb_inc;
+        rp.epoch = epoch;
+    }
+    ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
+    ProfSpan main(ctx, ZMQG_PROF_DECODE_MAIN, st);
+    launch_frames<true>(G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out, ctx->sessions,
+                        ctx->max_sessions, flags_out, status_out, rp,
+                        DecodeHead{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R},
+                        w.list_ctr + (par ^ 1u));
+    ZCHECK(ctx, hipGetLastError());
+    main.end();
+    if (multi) {
+        size_t tb = w.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(w.temp, tb, sid, w.keys_s, w.iota, w.perm, (int) nn, 0,
                                                         ctx->sort_bits, st));
         hipLaunchKernelGGL(k_gather_u64, hgrid, dim3(kHeadThreads), 0, st, nn, w.perm, w.v, w.v_s);
@@ -1552,14 +1596,17 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
                            w.last);
         ZCHECK(ctx, hipGetLastError());
     }
-    tb = w.temp_bytes;
-    ZCHECK(ctx, hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.nch, w.chunk_end, (int) nn, st));
     ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
-    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, nn, w.chunk_end, w.hot, w.pw,
-                       w.fin, w.powtab, flags_out, status_out, sid, ctx->max_sessions, ctx->peer, w.acc, w.cnt,
-                       w.excl, w.last);
+    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, R.list_ctr, w.chunk_end, w.hot,
+                       w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap);
     ZCHECK(ctx, hipGetLastError());
     body.end();
+    if (multi) {
+        hipLaunchKernelGGL(k_fixup, dim3((nn + kFixupThreads - 1) / kFixupThreads), dim3(kFixupThreads), 0, st, nn,
+                           kMaxFrameStream, w.v, w.psnap, w.excl, w.last, sid, ctx->max_sessions, wire_len, out_off,
+                           out, status_out, flags_out, ctx->peer);
+        ZCHECK(ctx, hipGetLastError());
+    }
     call.end();
     return 0;
 }

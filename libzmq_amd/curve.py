@@ -138,7 +138,10 @@ class CurveContext:
         return v.value
 
     # ---- profiling hooks (HIP events around the body kernels) ----
-    PROF_ENCODE_BODY, PROF_DECODE_BODY, PROF_ENCODE_CALL, PROF_DECODE_CALL = 0, 1, 2, 3
+    # zmqg_curve.h ZMQG_PROF_*: MAIN = the frame kernel (dominant kernel),
+    # CALL = the whole batch call, BODY = the chunked body kernel (big frames)
+    PROF_ENCODE_MAIN, PROF_DECODE_MAIN, PROF_ENCODE_CALL, PROF_DECODE_CALL = 0, 1, 2, 3
+    PROF_ENCODE_BODY, PROF_DECODE_BODY = 4, 5
 
     def set_profiling(self, enable):
         self._check(_lib.zmqg_ctx_set_profiling(self._ctx, int(bool(enable))), "zmqg_ctx_set_profiling")
