@@ -233,12 +233,12 @@ __device__ __forceinline__ void block_limbs(const uint32_t *w, int nb, uint32_t 
 // Replay rule of src/curve_mechanism_base.cpp:98-106 in the decode frame
 // kernel.  Per frame: the header-valid nonce vout (0 for a header failure)
 // and the session's peer nonce before the batch (psnap).
-//   One session (ticket != null): workgroups take their frames in ticket
+//   One session (lb_flag != null): workgroups take their frames in ticket
 //   order and run a decoupled look-back over the workgroup maxima of vout,
 //   so each frame knows excl = max of every earlier header-valid nonce in
 //   the batch; small frames apply the rule here, big frames get excl for
 //   the body's finisher, and the last workgroup writes the new peer nonce.
-//   Several sessions (ticket == null): iota for the sort-by-session path;
+//   Several sessions (lb_flag == null): iota for the sort-by-session path;
 //   the rule is applied by k_fixup / the body finisher.
 struct ReplayOut {
     unsigned long long *vout;
@@ -246,11 +246,21 @@ struct ReplayOut {
     uint32_t *iota;
     unsigned long long *peer; // read (psnap); one session: written by the last workgroup
     unsigned long long *excl; // one session: per frame, for the body finisher
-    uint32_t *ticket;         // one session: this call's workgroup ticket counter
-    uint32_t *ticket_next;    // ... and the next call's (cleared here)
-    unsigned long long *lb_flag, *lb_agg, *lb_inc; // look-back state per ticket
-    uint32_t epoch;           // call number (look-back flags of older calls are stale)
+    unsigned long long *lb_flag, *lb_agg, *lb_inc; // one session: look-back state per ticket
     uint32_t dbg;             // timing experiments only (tools/frames_bench): 1 no look-back, 2 no ticket
+};
+
+// Per-context device state that carries from one batch call to the next,
+// kept on the device so that a captured hipGraph of calls replays correctly:
+// the call epoch (look-back flags of older calls are stale; parity selects
+// the big-frame list counter), the workgroup ticket and done counters (the
+// last workgroup to finish resets them and advances the epoch).
+struct ZState {
+    uint32_t epoch;  // >= 1
+    uint32_t ticket;
+    uint32_t done;
+    uint32_t pad;
+    unsigned long long list_ctr[2]; // big frames << 40 | body chunks, by epoch parity
 };
 
 // Decoupled look-back, whole workgroup: maximum of the aggregates of every
@@ -322,38 +332,41 @@ __device__ __forceinline__ void lookback_publish(unsigned long long *flag, unsig
 
 // No big-frame handler (tools, tests): frames above max_stream are skipped.
 struct NoBigFrames {
-    __device__ void operator()(uint32_t) const {}
+    __device__ void operator()(uint32_t, unsigned long long *) const {}
 };
 
 // Frame kernel.  DEC = decode.  Frames whose stream is longer than
-// max_stream (with a valid header, for decode) are handed to `big(i)` on
-// one lane (the chunked path's head: block 0, records, list entry).
-// Workgroup 0 clears *zero_next (the next call's big-frame list counter).
+// max_stream (with a valid header, for decode) are handed to
+// `big(i, list_ctr)` on one lane (the chunked path's head: block 0, records,
+// an entry in this call's big-frame list).
+// zs: the context's call state (see ZState); decode with rp.lb_flag set
+// applies the one-session replay rule in this kernel.
 template <bool DEC, int G, class BigOp>
 __global__ __launch_bounds__(256) void k_frames(
     uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
     const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
     uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
-    ReplayOut rp, BigOp big, unsigned long long *__restrict__ zero_next)
+    ReplayOut rp, BigOp big, ZState *__restrict__ zs)
 {
     static_assert(G == 1 || G == 2 || G == 4, "lanes per frame");
-    const bool lb = DEC && rp.ticket != nullptr;
+    const bool lb = DEC && rp.lb_flag != nullptr;
     uint32_t wg = blockIdx.x;
-    __shared__ uint32_t sh_ticket;
+    __shared__ uint32_t sh_ticket, sh_epoch;
     __shared__ unsigned long long sh_wmax[4];
-    if (lb && !(rp.dbg & 2)) {
-        if (threadIdx.x == 0)
-            sh_ticket = atomicAdd(rp.ticket, 1u);
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        // the epoch first: it only advances after every workgroup has finished
+        sh_epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lb && !(rp.dbg & 2))
+            sh_ticket = atomicAdd(&zs->ticket, 1u);
+    }
+    __syncthreads();
+    const uint32_t epoch = sh_epoch;
+    if (lb && !(rp.dbg & 2))
         wg = sh_ticket;
-    }
-    if (wg == 0 && threadIdx.x == 0) {
-        if (zero_next)
-            *zero_next = 0;
-        if (lb)
-            *rp.ticket_next = 0;
-    }
+    unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        zs->list_ctr[(epoch & 1u) ^ 1u] = 0; // the next call's list (the previous body has finished with it)
     const uint32_t gl = wg * 256u + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t i = gl / G, q = gl % G;
@@ -434,25 +447,10 @@ __global__ __launch_bounds__(256) void k_frames(
             if (lane > 0)
                 wexcl = up > wexcl ? up : wexcl;
             if (threadIdx.x == 0)
-                lookback_publish(rp.lb_flag + wg, rp.lb_agg + wg, wagg, rp.epoch, 1);
+                lookback_publish(rp.lb_flag + wg, rp.lb_agg + wg, wagg, epoch, 1);
         }
     }
-    // replay: this workgroup's exclusive prefix (every earlier frame's
-    // header-valid nonce) from the look-back, published as soon as known
-    unsigned long long excl = 0;
-    if (lb) {
-        const unsigned long long P =
-            (rp.dbg & 1) ? 0ull : lookback_excl(wg, rp.epoch, rp.lb_flag, rp.lb_agg, rp.lb_inc);
-        if (threadIdx.x == 0) {
-            const unsigned long long inc = P > wagg ? P : wagg;
-            lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, rp.epoch, 2);
-            if (wg + 1 == gridDim.x) // _cn_peer_nonce after the batch
-                *rp.peer = inc > psn ? inc : psn;
-        }
-        excl = P > wexcl ? P : wexcl;
-        if (excl < psn)
-            excl = psn;
-    }
+
     const bool is_big = valid && !small && S > 0;
     if (!small)
         S = 0; // nothing for this lane
@@ -690,10 +688,39 @@ __global__ __launch_bounds__(256) void k_frames(
 #pragma unroll
         for (int k = 0; k < 5; ++k)
             tot[k] += (uint32_t) __shfl_xor((int) tot[k], d);
+    // replay: this workgroup's exclusive prefix (every earlier frame's
+    // header-valid nonce) from the look-back -- at the end, when the earlier
+    // workgroups' aggregates (published after their header pass) are long
+    // visible and most have published their inclusive values
+    unsigned long long excl = 0;
+    if (lb) {
+        const unsigned long long P =
+            (rp.dbg & 1) ? 0ull : lookback_excl(wg, epoch, rp.lb_flag, rp.lb_agg, rp.lb_inc);
+        if (threadIdx.x == 0) {
+            const unsigned long long inc = P > wagg ? P : wagg;
+            lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
+            if (wg + 1 == gridDim.x) // _cn_peer_nonce after the batch
+                *rp.peer = inc > psn ? inc : psn;
+        }
+        excl = P > wexcl ? P : wexcl;
+        if (excl < psn)
+            excl = psn;
+    }
     if (is_big && q == 0) {
         if (lb)
             rp.excl[i] = excl;
-        big(i);
+        big(i, list_ctr);
+    }
+    // the last workgroup to get here resets the counters and advances the
+    // epoch for the next call (every workgroup has read epoch and ticket)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this workgroup's list appends are done
+        if (atomicAdd(&zs->done, 1u) + 1u == gridDim.x) {
+            __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     if (!valid || q != 0 || !small)
         return;

@@ -34,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -132,8 +133,7 @@ struct Workspace {
     uint32_t *list_frame = nullptr;      // [cap] big-frame list: frame index at each position
     unsigned long long *psnap = nullptr; // [cap] session peer nonce before the batch, per frame
     unsigned long long *blockmax = nullptr; // [cap] frame-kernel workgroup maxima of vout
-    unsigned long long *list_ctr = nullptr; // [2] big frames << 40 | body chunks, by call parity
-    uint32_t *ticket = nullptr;             // [2] frame-kernel workgroup tickets, by call parity
+    ZState *zs = nullptr;                   // call state carried from call to call (on the device)
     unsigned long long *lb_flag = nullptr;  // [cap] look-back state per workgroup ticket
     unsigned long long *lb_agg = nullptr;   // [cap]
     unsigned long long *lb_inc = nullptr;   // [cap]
@@ -160,7 +160,6 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
-    uint32_t calls = 0; // batch calls so far: list/ticket parity, look-back epoch
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
     char last_error[256] = {0};
@@ -306,7 +305,6 @@ struct BigRecords {
     uint32_t *powtab;
     unsigned long long *acc;
     uint32_t *cnt;
-    unsigned long long *list_ctr; // this call's big-frame list counter
     uint32_t *chunk_end;
     uint32_t *list_frame;
 };
@@ -326,10 +324,10 @@ struct EncodeHead {
     const DevSession *sessions;
     uint32_t max_sessions;
     BigRecords R;
-    __device__ void operator()(uint32_t i) const;
+    __device__ void operator()(uint32_t i, unsigned long long *list_ctr) const;
 };
 
-__device__ void EncodeHead::operator()(uint32_t i) const
+__device__ void EncodeHead::operator()(uint32_t i, unsigned long long *list_ctr) const
 {
     FrameHot *hot = R.hot;
     FramePow *pw = R.pw;
@@ -345,7 +343,7 @@ __device__ void EncodeHead::operator()(uint32_t i) const
     const uint32_t mlen = hl + P;
     uint32_t nch, blast;
     body_geometry(mlen, nch, blast);
-    const uint32_t p = list_append(R.list_ctr, R.chunk_end, R.list_frame, i, nch);
+    const uint32_t p = list_append(list_ctr, R.chunk_end, R.list_frame, i, nch);
     FrameHot H;
 #pragma unroll
     for (int t = 0; t < 8; ++t)
@@ -483,10 +481,10 @@ struct DecodeHead {
     const DevSession *sessions;
     uint32_t max_sessions;
     BigRecords R;
-    __device__ void operator()(uint32_t i) const;
+    __device__ void operator()(uint32_t i, unsigned long long *list_ctr) const;
 };
 
-__device__ void DecodeHead::operator()(uint32_t i) const
+__device__ void DecodeHead::operator()(uint32_t i, unsigned long long *list_ctr) const
 {
     FrameHot *hot = R.hot;
     FramePow *pw = R.pw;
@@ -503,7 +501,7 @@ __device__ void DecodeHead::operator()(uint32_t i) const
     const uint32_t mlen = wl - 32;
     uint32_t nch, blast;
     body_geometry(mlen, nch, blast);
-    const uint32_t p = list_append(R.list_ctr, R.chunk_end, R.list_frame, i, nch);
+    const uint32_t p = list_append(list_ctr, R.chunk_end, R.list_frame, i, nch);
 #pragma unroll
     for (int t = 0; t < 5; ++t)
         acc[(size_t) p * 5 + t] = 0;
@@ -920,11 +918,11 @@ __device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t
     }
 }
 
-// The big-frame list (positions 0 .. n-1, written by the head kernel) is
-// read from *list_ctr: n = entries, total = body chunks.
+// The big-frame list (positions 0 .. n-1, built by the frame kernel's head
+// calls) is read from the call state: n = entries, total = body chunks.
 template <bool DEC>
 __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_body(
-    const unsigned long long *__restrict__ list_ctr, const uint32_t *__restrict__ chunk_end,
+    const ZState *__restrict__ zs, const uint32_t *__restrict__ chunk_end,
     const FrameHot *__restrict__ hot, const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
     const uint32_t *__restrict__ powtab, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
     unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
@@ -933,7 +931,8 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
     __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kBufLds];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t *const wlds = lds + wv * 2 * kBufLds;
-    const unsigned long long lc = *list_ctr;
+    // the frame kernel before this one advanced the epoch: its list is parity epoch-1
+    const unsigned long long lc = zs->list_ctr[(zs->epoch - 1u) & 1u];
     const uint32_t n = (uint32_t) (lc >> 40), total = (uint32_t) (lc & ((1ull << 40) - 1));
     if (n == 0)
         return;
@@ -1198,11 +1197,12 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
             (rc = grow(ctx, w.lb_inc, cap)))
             return rc;
         ZCHECK(ctx, hipMemset(w.lb_flag, 0, cap * sizeof(unsigned long long)));
-        if (!w.list_ctr) {
-            if ((rc = grow(ctx, w.list_ctr, 2)) || (rc = grow(ctx, w.ticket, 2)))
+        if (!w.zs) {
+            if ((rc = grow(ctx, w.zs, 1)))
                 return rc;
-            ZCHECK(ctx, hipMemset(w.list_ctr, 0, 2 * sizeof(unsigned long long)));
-            ZCHECK(ctx, hipMemset(w.ticket, 0, 2 * sizeof(uint32_t)));
+            ZState z0{};
+            z0.epoch = 1;
+            ZCHECK(ctx, hipMemcpy(w.zs, &z0, sizeof z0, hipMemcpyHostToDevice));
         }
         w.cap = cap;
     }
@@ -1292,12 +1292,12 @@ template <bool DEC, class BigOp>
 void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const uint64_t *nonce,
                    const uint8_t *flags, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
                    const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
-                   uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, unsigned long long *zero_next)
+                   uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs)
 {
     const dim3 grid((uint32_t) (((uint64_t) n * G + 255) / 256));
 #define ZMQG_LAUNCH_FRAMES(GG)                                                                                        \
     hipLaunchKernelGGL((k_frames<DEC, GG, BigOp>), grid, dim3(256), 0, st, n, sid, nonce, flags, in_off, len, in,      \
-                       out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zero_next)
+                       out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs)
     if (G == 1)
         ZMQG_LAUNCH_FRAMES(1);
     else if (G == 2)
@@ -1361,8 +1361,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     (void) hipDeviceSynchronize();
     Workspace &w = ctx->ws;
     void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
-                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.psnap, w.blockmax, w.list_ctr,
-                    w.ticket, w.lb_flag, w.lb_agg, w.lb_inc, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
+                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.psnap, w.blockmax, w.zs,
+                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
             (void) hipFree(p);
@@ -1517,19 +1517,18 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     Workspace &w = ctx->ws;
     const uint32_t nn = (uint32_t) n;
     const int G = lanes_per_frame(nn);
-    const uint32_t par = ctx->calls++ & 1u;
-    const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.list_ctr + par, w.chunk_end, w.list_frame};
+    const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_ENCODE_MAIN, st);
     launch_frames<false>(G, nn, st, sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
                          ctx->max_sessions, nullptr, nullptr, ReplayOut{},
                          EncodeHead{sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
                                     ctx->max_sessions, R},
-                         w.list_ctr + (par ^ 1u));
+                         w.zs);
     ZCHECK(ctx, hipGetLastError());
     main.end();
     ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
-    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, R.list_ctr, w.chunk_end, w.hot,
+    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
                        w.pw, w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, w.acc, w.cnt,
                        (const unsigned long long *) nullptr, (const unsigned long long *) nullptr);
     ZCHECK(ctx, hipGetLastError());
@@ -1558,8 +1557,7 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     const dim3 hgrid((nn + kHeadThreads - 1) / kHeadThreads);
     const int G = lanes_per_frame(nn);
     const bool multi = ctx->sort_bits > 0;
-    const uint32_t par = ctx->calls++ & 1u, epoch = ctx->calls; // epoch >= 1
-    const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.list_ctr + par, w.chunk_end, w.list_frame};
+    const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ReplayOut rp{};
     rp.vout = w.v;
     rp.psnap = w.psnap;
@@ -1568,19 +1566,18 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         rp.iota = w.iota;
     } else {
         rp.excl = w.excl;
-        rp.ticket = w.ticket + par;
-        rp.ticket_next = w.ticket + (par ^ 1u);
         rp.lb_flag = w.lb_flag;
         rp.lb_agg = w.lb_agg;
         rp.lb_inc = w.lb_inc;
-        rp.epoch = epoch;
+        static const char *dbg = getenv("ZMQG_LB_DBG"); // timing experiments only
+        rp.dbg = dbg ? (uint32_t) atoi(dbg) : 0u;
     }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_DECODE_MAIN, st);
     launch_frames<true>(G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out, ctx->sessions,
                         ctx->max_sessions, flags_out, status_out, rp,
                         DecodeHead{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R},
-                        w.list_ctr + (par ^ 1u));
+                        w.zs);
     ZCHECK(ctx, hipGetLastError());
     main.end();
     if (multi) {
@@ -1597,7 +1594,7 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         ZCHECK(ctx, hipGetLastError());
     }
     ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
-    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, R.list_ctr, w.chunk_end, w.hot,
+    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
                        w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap);
     ZCHECK(ctx, hipGetLastError());
     body.end();

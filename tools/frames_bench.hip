@@ -107,6 +107,13 @@ int main(int argc, char **argv)
     std::vector<uint8_t> h_ref(wb), h_new(wb), h_back(pay.size());
     CHECK(hipMemcpy(h_ref.data(), d_ref, wb, hipMemcpyDeviceToHost));
     printf("n=%u P=%u library encode %.1f us\n", n, P, t_ref);
+    ZState *d_zs;
+    CHECK(hipMalloc(&d_zs, sizeof(ZState)));
+    {
+        ZState z0{};
+        z0.epoch = 1;
+        CHECK(hipMemcpy(d_zs, &z0, sizeof z0, hipMemcpyHostToDevice));
+    }
     ReplayOut rpo{};
     rpo.vout = d_v;
     rpo.psnap = d_v + n;
@@ -117,7 +124,7 @@ int main(int argc, char **argv)
         CHECK(hipMemset(d_wire, 0, wb));
         double te = timeit([&] {
             hipLaunchKernelGGL(kenc, dim3(blocks), dim3(256), 0, 0, n, d_sid, d_nonce, d_flags, d_ioff, d_len, d_pay,
-                               d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr, ReplayOut{}, NoBigFrames{}, nullptr);
+                               d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr, ReplayOut{}, NoBigFrames{}, d_zs);
         });
         CHECK(hipMemcpy(h_new.data(), d_wire, wb, hipMemcpyDeviceToHost));
         size_t bad = 0, first = (size_t) -1;
@@ -128,7 +135,7 @@ int main(int argc, char **argv)
         double td = timeit([&] {
             hipLaunchKernelGGL(kdec, dim3(blocks), dim3(256), 0, 0, n, d_sid, (const uint64_t *) nullptr,
                                (const uint8_t *) nullptr, d_ooff, d_wl, d_ref, d_ioff, d_back, d_ses, 1u, 0xffffffffu,
-                               d_fl, d_st, rpo, NoBigFrames{}, nullptr);
+                               d_fl, d_st, rpo, NoBigFrames{}, d_zs);
         });
         CHECK(hipMemcpy(h_back.data(), d_back, pay.size(), hipMemcpyDeviceToHost));
         std::vector<int32_t> st(n);
@@ -156,22 +163,17 @@ int main(int argc, char **argv)
         CHECK(hipMemset(lbf, 0, 8 * n));
         CHECK(hipMemset(tk, 0, 8));
         const uint32_t blocks = (uint32_t) (((uint64_t) n * 2 + 255) / 256);
-        uint32_t epoch = 0, par = 0;
         for (uint32_t dbg : {3u, 2u, 1u, 0u}) {
         double td = timeit([&] {
             ReplayOut r = rpo;
             r.dbg = dbg;
             r.excl = ex;
-            r.ticket = tk + par;
-            r.ticket_next = tk + (par ^ 1);
             r.lb_flag = lbf;
             r.lb_agg = lba;
             r.lb_inc = lbi;
-            r.epoch = ++epoch;
-            par ^= 1;
             hipLaunchKernelGGL((k_frames<true, 2, NoBigFrames>), dim3(blocks), dim3(256), 0, 0, n, d_sid,
                                (const uint64_t *) nullptr, (const uint8_t *) nullptr, d_ooff, d_wl, d_ref, d_ioff,
-                               d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, r, NoBigFrames{}, nullptr);
+                               d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, r, NoBigFrames{}, d_zs);
         });
         printf("dbg=%u: %.1f us\n", dbg, td);
         }
