@@ -404,3 +404,62 @@ def test_host_path_matches_device_path(torch_cuda, C):
     a = ctx.encode_host(b["sid"], b["nonce"], b["flags"], b["in_off"], b["lens"], b["inp"], out_off, total)
     d = gpu_encode(torch_cuda, ctx, b, out_off, total)
     assert np.array_equal(a, d)
+
+
+@pytest.mark.parametrize("n,sizes", [(3000, [0, 7, 64, 200, 1024, 6000]), (40000, [0, 9, 100]),
+                                     (140000, [1, 30])])
+def test_replay_single_session_lookback(torch_cuda, C, n, sizes):
+    """One session: the replay rule runs inside the frame kernel (decoupled
+    look-back over workgroup tickets) and in the body finisher for frames
+    above the frame kernel's limit.  Duplicates, reorders, header and MAC
+    failures scattered over many workgroups (G = 4, 2 and 1 lanes per frame
+    at these batch sizes): statuses, flags, payloads and the new peer nonce
+    equal the reference's sequential rule (oracle)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(n)
+    precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc = C.CurveContext(0, 1)
+    enc.session_set(0, precom, O.CLIENT_PREFIX, O.SERVER_PREFIX)
+    m = n - n // 20
+    b = random_batch(rng, m, sizes, 1)
+    out_off, wl, total = wire_layout(b["flags"], b["lens"], [False], b["sid"])
+    wire = gpu_encode(torch, enc, b, out_off, total)
+    frames = [wire[int(out_off[i]):int(out_off[i]) + int(wl[i])].tobytes() for i in range(m)]
+    stream = []
+    for i in range(m):
+        r = rng.random()
+        if r < 0.02 and stream:  # replay an earlier frame
+            stream.append(stream[int(rng.integers(0, len(stream)))])
+        elif r < 0.03:  # swap with the next frame (the later one arrives first)
+            if i + 1 < m:
+                stream.append(frames[i + 1])
+        elif r < 0.04:  # tampered ciphertext
+            f = bytearray(frames[i])
+            f[-1] ^= 0x01
+            stream.append(bytes(f))
+        elif r < 0.045:  # not a MESSAGE command
+            f = bytearray(frames[i])
+            f[3] ^= 0x20
+            stream.append(bytes(f))
+        stream.append(frames[i])
+    stream = stream[:n]
+    inp, in_off = pack(stream, rng, 3)
+    wls = np.array([len(f) for f in stream], np.uint32)
+    plen = np.maximum(wls.astype(np.int64) - 33, 0)
+    _, pout = pack([b"\0" * int(p) for p in plen])
+    psize = int(pout[-1]) + int(plen[-1]) + 1
+    dec = C.CurveContext(0, 1)
+    dec.session_set(0, precom, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    sid = np.zeros(len(stream), np.uint32)
+    pl, fl, st = gpu_decode(torch, dec, sid, in_off, wls, inp, pout, psize)
+    peer = np.array([2], np.uint64)
+    rpl, rfl, rst = O.decode_batch(O.make_sessions([precom], dec_prefix=O.CLIENT_PREFIX), peer, sid, in_off, wls,
+                                   inp, pout, psize)
+    assert (rst == C.ERR_INVALID_SEQUENCE).any() and (rst == C.ERR_CRYPTOGRAPHIC).any()
+    assert np.array_equal(st, rst)
+    assert np.array_equal(fl, rfl)
+    assert np.array_equal(pl, rpl)
+    assert dec.get_peer_nonce(0) == int(peer[0])
+    # a second batch on the same context continues from the new peer nonce
+    pl2, fl2, st2 = gpu_decode(torch, dec, sid[:50], in_off[:50], wls[:50], inp, pout[:50], psize)
+    assert (st2 != 0).all() and (st2 == C.ERR_INVALID_SEQUENCE).sum() >= 40
