@@ -248,6 +248,7 @@ struct ReplayOut {
     unsigned long long *excl; // one session: per frame, for the body finisher
     unsigned long long *lb_flag, *lb_agg, *lb_inc; // one session: look-back state per ticket
     uint32_t dbg;             // timing experiments only (tools/frames_bench): 1 no look-back, 2 no ticket
+    unsigned long long *clk;  // diagnostics only: per workgroup {start, end} s_memrealtime, memtime delta, hw ids
 };
 
 // Per-context device state that carries from one batch call to the next,
@@ -351,6 +352,11 @@ __global__ __launch_bounds__(256) void k_frames(
 {
     static_assert(G == 1 || G == 2 || G == 4, "lanes per frame");
     const bool lb = DEC && rp.lb_flag != nullptr;
+    unsigned long long clk0 = 0, rclk0 = 0;
+    if (rp.clk) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        rclk0 = __builtin_amdgcn_s_memrealtime();
+    }
     uint32_t wg = blockIdx.x;
     __shared__ uint32_t sh_ticket, sh_epoch;
     __shared__ unsigned long long sh_wmax[4];
@@ -475,14 +481,31 @@ __global__ __launch_bounds__(256) void k_frames(
     bool hasH = false;
     uint32_t lastH = 0; // window index of the lane's last window below L
     uint32_t ycarry = 0; // word 15 of window (this lane's window - 1), for q == 0
-    uint32_t dn[17];
+    uint32_t dn[17]; // raw input words of this lane's next window, loaded a step ahead
     if (nst > 0 && !(q == 0 && !DEC)) // encode's window 0 reads the payload itself
         frame_load_raw(A, q, S, dn);
 
 #pragma unroll 1
     for (uint32_t t = 0; t < steps; ++t) {
+        // Progress-based issue priority: the two waves on a SIMD share its
+        // VALU, which favours the older wave; a wave that is ahead drops its
+        // priority so both finish together instead of the younger one
+        // running its last third alone (latency-bound).
+        if (4 * t < steps)
+            __builtin_amdgcn_s_setprio(3);
+        else if (2 * t < steps)
+            __builtin_amdgcn_s_setprio(2);
+        else if (4 * t < 3 * steps)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
         const uint32_t w = t * G + q;
         const bool act = w < nw;
+        // the keystream first: it needs no input, so the wait for this
+        // step's words (and, vmcnt being in order, for the previous step's
+        // stores issued after them) comes after ~1000 instructions of Salsa20
+        uint32_t ks[16];
+        salsa20_block(ks, key, n0, n1, w, 0);
         uint32_t dc[17];
 #pragma unroll
         for (int k = 0; k < 17; ++k)
@@ -514,8 +537,6 @@ __global__ __launch_bounds__(256) void k_frames(
         } else {
             frame_words(dc, vin, w, S, x);
         }
-        uint32_t ks[16];
-        salsa20_block(ks, key, n0, n1, w, 0);
         // r from keystream block 0 (lane 0 of the group) to the group
         if (t == 0) {
             const fe r0 = poly_r_from_key(ks[0], ks[1], ks[2], ks[3]);
@@ -710,6 +731,14 @@ __global__ __launch_bounds__(256) void k_frames(
         if (lb)
             rp.excl[i] = excl;
         big(i, list_ctr);
+    }
+    if (rp.clk && threadIdx.x == 0) {
+        unsigned long long *c = rp.clk + 4ull * blockIdx.x;
+        c[0] = rclk0;
+        c[1] = __builtin_amdgcn_s_memrealtime();
+        c[2] = __builtin_amdgcn_s_memtime() - clk0;
+        c[3] = ((unsigned long long) __builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+               __builtin_amdgcn_s_getreg((31 << 11) | 4); // XCC_ID : HW_ID
     }
     // the last workgroup to get here resets the counters and advances the
     // epoch for the next call (every workgroup has read epoch and ticket)

@@ -114,17 +114,21 @@ int main(int argc, char **argv)
         z0.epoch = 1;
         CHECK(hipMemcpy(d_zs, &z0, sizeof z0, hipMemcpyHostToDevice));
     }
+    unsigned long long *d_clk;
+    CHECK(hipMalloc(&d_clk, 32 * 4096));
     ReplayOut rpo{};
+    rpo.clk = d_clk;
     rpo.vout = d_v;
     rpo.psnap = d_v + n;
     rpo.peer = d_v + 3 * n;
     int fails = 0;
     auto run = [&](auto kenc, auto kdec, int G) {
+        CHECK(hipMemset(d_clk, 0, 32 * 4096));
         const uint32_t blocks = (uint32_t) (((uint64_t) n * G + 255) / 256);
         CHECK(hipMemset(d_wire, 0, wb));
         double te = timeit([&] {
             hipLaunchKernelGGL(kenc, dim3(blocks), dim3(256), 0, 0, n, d_sid, d_nonce, d_flags, d_ioff, d_len, d_pay,
-                               d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr, ReplayOut{}, NoBigFrames{}, d_zs);
+                               d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr, rpo, NoBigFrames{}, d_zs);
         });
         CHECK(hipMemcpy(h_new.data(), d_wire, wb, hipMemcpyDeviceToHost));
         size_t bad = 0, first = (size_t) -1;
@@ -147,6 +151,33 @@ int main(int argc, char **argv)
             bad2 += h_back[k] != pay[k];
         for (uint32_t k = 0; k < n; ++k)
             bads += st[k] != 0 || fl[k] != flags[k];
+        {
+            const uint32_t nwg = blocks;
+            std::vector<unsigned long long> ck(4 * nwg);
+            CHECK(hipMemcpy(ck.data(), d_clk, 32 * nwg, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull, t1 = 0;
+            for (uint32_t w = 0; w < nwg; ++w) {
+                t0 = ck[4 * w] < t0 ? ck[4 * w] : t0;
+                t1 = ck[4 * w + 1] > t1 ? ck[4 * w + 1] : t1;
+            }
+            char fn[64];
+            snprintf(fn, sizeof fn, "gpurun_out/wg_G%d.csv", G);
+            FILE *f = fopen(fn, "w");
+            double dsum = 0, dmax = 0, smax = 0;
+            for (uint32_t w = 0; w < nwg; ++w) {
+                const double st = (ck[4 * w] - t0) / 100.0, du = (ck[4 * w + 1] - ck[4 * w]) / 100.0;
+                dsum += du;
+                dmax = du > dmax ? du : dmax;
+                smax = st > smax ? st : smax;
+                if (f)
+                    fprintf(f, "%u,%.2f,%.2f,%llu,%llu,%llu\n", w, st, du, ck[4 * w + 2], ck[4 * w + 3] >> 32,
+                            ck[4 * w + 3] & 0xffffffffull);
+            }
+            if (f)
+                fclose(f);
+            printf("   decode workgroups: span %.1f us, mean %.1f us, max %.1f us, latest start %.1f us\n",
+                   (t1 - t0) / 100.0, dsum / nwg, dmax, smax);
+        }
         printf("G=%d encode %.1f us (%.0f GB/s payload) mismatched %zu (first %zd) | decode %.1f us (%.0f GB/s) payload mismatches %zu status/flag %zu\n",
                G, te, (double) n * P / te / 1e3, bad, (ssize_t) first, td, (double) n * P / td / 1e3, bad2, bads);
         fails += bad || bad2 || bads;
