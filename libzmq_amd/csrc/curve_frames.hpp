@@ -247,6 +247,8 @@ struct ReplayOut {
     unsigned long long *peer; // read (psnap); one session: written by the last workgroup
     unsigned long long *excl; // one session: per frame, for the body finisher
     unsigned long long *lb_flag, *lb_agg, *lb_inc; // one session: look-back state per ticket
+    uint32_t ordered;         // 1: the whole grid is co-resident, so workgroups use blockIdx as
+                              //    their look-back order (no ticket)
     uint32_t dbg;             // timing experiments only (tools/frames_bench): 1 no look-back, 2 no ticket
     unsigned long long *clk;  // diagnostics only: per workgroup {start, end} s_memrealtime, memtime delta, hw ids
 };
@@ -363,12 +365,12 @@ __global__ __launch_bounds__(256) void k_frames(
     if (threadIdx.x == 0) {
         // the epoch first: it only advances after every workgroup has finished
         sh_epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lb && !(rp.dbg & 2))
+        if (lb && !rp.ordered && !(rp.dbg & 2))
             sh_ticket = atomicAdd(&zs->ticket, 1u);
     }
     __syncthreads();
     const uint32_t epoch = sh_epoch;
-    if (lb && !(rp.dbg & 2))
+    if (lb && !rp.ordered && !(rp.dbg & 2))
         wg = sh_ticket;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)

@@ -160,6 +160,7 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
+    int frames_cap[3] = {0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
     char last_error[256] = {0};
@@ -1288,6 +1289,22 @@ int lanes_per_frame(uint32_t n)
     return n >= 131072u ? 1 : n >= 32768u ? 2 : 4;
 }
 
+// Workgroups of the decode frame kernel the device holds at once (occupancy
+// query x CUs; the kernel is VGPR-limited, where the query is exact --
+// MI355X_MICROARCH.md, Residency), cached per G.
+int frames_capacity(zmqg_ctx *ctx, int G)
+{
+    int &c = ctx->frames_cap[G == 1 ? 0 : G == 2 ? 1 : 2];
+    if (c == 0) {
+        int nb = 0;
+        hipError_t e = G == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, 256, 0)
+                       : G == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, 256, 0)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 4, DecodeHead>, 256, 0);
+        c = (e == hipSuccess && nb > 0) ? nb * ctx->cus : -1;
+    }
+    return c;
+}
+
 template <bool DEC, class BigOp>
 void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const uint64_t *nonce,
                    const uint8_t *flags, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
@@ -1569,8 +1586,11 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         rp.lb_flag = w.lb_flag;
         rp.lb_agg = w.lb_agg;
         rp.lb_inc = w.lb_inc;
-        static const char *dbg = getenv("ZMQG_LB_DBG"); // timing experiments only
-        rp.dbg = dbg ? (uint32_t) atoi(dbg) : 0u;
+        // A grid that fits the device at once can use blockIdx as the
+        // look-back order (every workgroup becomes resident eventually,
+        // whatever the dispatch order); a larger one takes tickets.
+        const uint64_t grid = ((uint64_t) nn * G + 255) / 256;
+        rp.ordered = grid <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
     }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_DECODE_MAIN, st);
