@@ -65,6 +65,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    # one process per GPU; (a rehearsal with more ranks than GPUs shares them)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -165,10 +167,8 @@ def main():
             step(stream)
         torch.cuda.synchronize(dev)
         eager_elapsed = time.perf_counter() - e0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    from libzmq_amd import shard
+    elapsed = shard.max_over_ranks(elapsed)  # the slowest rank times the job
     # (with a graph, the event pairs recorded at capture now hold the timed
     # replay's timestamps: every replay re-records them)
     enc_body_ms, enc_body_n = enc.get_profile(C.CurveContext.PROF_ENCODE_MAIN)
