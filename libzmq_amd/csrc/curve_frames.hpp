@@ -37,6 +37,10 @@
 // neighbouring frames are never touched.
 #pragma once
 
+#ifndef ZMQG_FRAMES_ABLATE
+#define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: 1 no Poly1305, 2 no stores, 4 no input shift
+#endif
+
 #include "../../include/zmqg_curve.h"
 #include "curve_device.hpp"
 
@@ -537,7 +541,13 @@ __global__ __launch_bounds__(256) void k_frames(
             if (S < 64u)
                 mask_tail(x, (int) S);
         } else {
-            frame_words(dc, vin, w, S, x);
+            if (ZMQG_FRAMES_ABLATE & 4) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    x[k] = dc[k];
+            } else {
+                frame_words(dc, vin, w, S, x);
+            }
         }
         // r from keystream block 0 (lane 0 of the group) to the group
         if (t == 0) {
@@ -593,7 +603,13 @@ __global__ __launch_bounds__(256) void k_frames(
         }
         if (act) {
             // Poly1305 contribution of this window
-            if (w < L) {
+            if (ZMQG_FRAMES_ABLATE & 1) {
+                if (w < L) {
+                    H[0] ^= c[0] ^ c[7] ^ c[13];
+                    hasH = true;
+                    lastH = w;
+                }
+            } else if (w < L) {
                 uint64_t a[5];
                 if (hasH) {
 #pragma unroll
@@ -689,7 +705,10 @@ __global__ __launch_bounds__(256) void k_frames(
         const uint32_t fromleft = (uint32_t) __shfl((int) y15, (int) (lane > 0 ? lane - 1 : 0));
         const uint32_t yprev = q == 0 ? ycarry : fromleft;
         if (act && w > 0)
-            frame_store(B, w, S, y, yprev, w == L);
+            if (!(ZMQG_FRAMES_ABLATE & 2))
+                frame_store(B, w, S, y, yprev, w == L);
+            else
+                *(GU32 *) (uintptr_t) (B + 64ull * w) = y[0] ^ y[5] ^ y[9] ^ y[15] ^ yprev;
         ycarry = (uint32_t) __shfl((int) y15, (int) (gbase + G - 1));
     }
     // H_q * r^(kb + 4(L-1-lastH)), plus U'_L (already in tot)

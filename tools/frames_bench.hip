@@ -182,6 +182,16 @@ int main(int argc, char **argv)
                G, te, (double) n * P / te / 1e3, bad, (ssize_t) first, td, (double) n * P / td / 1e3, bad2, bads);
         fails += bad || bad2 || bads;
     };
+    if (getenv("FB_ENC2_ONLY")) { // instruction-count experiments: the G = 2 encode kernel alone
+        const uint32_t blocks = (uint32_t) (((uint64_t) n * 2 + 255) / 256);
+        double te = timeit([&] {
+            hipLaunchKernelGGL((k_frames<false, 2, NoBigFrames>), dim3(blocks), dim3(256), 0, 0, n, d_sid, d_nonce,
+                               d_flags, d_ioff, d_len, d_pay, d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr,
+                               rpo, NoBigFrames{}, d_zs);
+        });
+        printf("G=2 encode only: %.1f us\n", te);
+        return 0;
+    }
     {
         // single-session replay in-kernel (decoupled look-back), G = 2
         unsigned long long *lbf, *lba, *lbi, *ex;
