@@ -138,6 +138,33 @@ int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
                      const uint32_t *wire_len, const uint8_t *in, uint64_t in_bytes, const uint64_t *out_off,
                      uint8_t *out, uint64_t out_bytes, uint8_t *flags_out, int32_t *status_out);
 
+/* Asynchronous host path.  The reference's
+ * engine encodes and decodes one message at a time on the I/O thread
+ * (src/stream_engine_base.cpp:281-291 in_event, :331-348 out_event); an
+ * engine that batches across its connections instead needs host memory the
+ * kernels can work on in place and a way to learn, without blocking, that a
+ * submitted batch is finished.
+ *
+ * zmqg_host_alloc returns page-locked host memory mapped into the device's
+ * address space: batch calls take pointers into it directly (descriptors,
+ * `in`, `out`, flags_out, status_out) and the kernels read and write it over
+ * PCIe with no staging copy.  Free it with zmqg_host_free (after the batches
+ * using it have finished).
+ *
+ * zmqg_ctx_stream gives the ctx's own non-blocking stream for callers without
+ * one.  zmqg_fence_record marks the point after everything issued so far on
+ * `stream` and returns a fence id (ids increase per ctx); zmqg_fence_query
+ * returns 1 once the stream has passed it, 0 while it has not (never
+ * blocks), and zmqg_fence_wait blocks until it has.  A fence is released by
+ * the first query or wait that finds it reached; later queries of a released
+ * or unknown id below the last issued one return 1. */
+int zmqg_host_alloc(zmqg_ctx *ctx, uint64_t bytes, void **ptr_out);
+int zmqg_host_free(zmqg_ctx *ctx, void *ptr);
+int zmqg_ctx_stream(zmqg_ctx *ctx, void **stream_out);
+int zmqg_fence_record(zmqg_ctx *ctx, void *stream, uint64_t *fence_out);
+int zmqg_fence_query(zmqg_ctx *ctx, uint64_t fence);
+int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
+
 /* Profiling hooks (off by default).  When enabled, the ctx records a HIP
  * event pair on the batch's stream around each of its kernels of one kind:
  *   ZMQG_PROF_ENCODE_MAIN / ZMQG_PROF_DECODE_MAIN  the frame kernel alone

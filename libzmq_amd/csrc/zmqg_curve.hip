@@ -163,6 +163,12 @@ struct zmqg_ctx {
     int frames_cap[3] = {0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
+    // completion fences of the asynchronous host path: (id, event) pending,
+    // events recycled through fence_pool
+    std::vector<std::pair<uint64_t, hipEvent_t>> fences;
+    std::vector<hipEvent_t> fence_pool;
+    uint64_t fence_ctr = 0;
+    std::mutex fence_mu;
     char last_error[256] = {0};
     std::mutex mu;
 };
@@ -1394,6 +1400,10 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
         }
     for (hipEvent_t e : ctx->event_pool)
         (void) hipEventDestroy(e);
+    for (auto &f : ctx->fences)
+        (void) hipEventDestroy(f.second);
+    for (hipEvent_t e : ctx->fence_pool)
+        (void) hipEventDestroy(e);
     delete ctx;
     return 0;
 }
@@ -1743,6 +1753,96 @@ int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     memcpy(flags_out, h + o_fl, n);
     memcpy(status_out, h + o_st, 4 * n);
     return 0;
+}
+
+int zmqg_host_alloc(zmqg_ctx *ctx, uint64_t bytes, void **ptr_out)
+{
+    if (!ctx || !ptr_out || bytes == 0)
+        return -EINVAL;
+    *ptr_out = nullptr;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    // page-locked and mapped; coherent (fine-grained), so kernel writes are
+    // visible to the host once a fence behind the batch has been reached
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+        return -ENOMEM;
+    ZCHECK(ctx, e);
+    *ptr_out = p;
+    return 0;
+}
+
+int zmqg_host_free(zmqg_ctx *ctx, void *ptr)
+{
+    if (!ctx || !ptr)
+        return -EINVAL;
+    ZCHECK(ctx, hipHostFree(ptr));
+    return 0;
+}
+
+int zmqg_ctx_stream(zmqg_ctx *ctx, void **stream_out)
+{
+    if (!ctx || !stream_out)
+        return -EINVAL;
+    *stream_out = (void *) ctx->own_stream;
+    return 0;
+}
+
+int zmqg_fence_record(zmqg_ctx *ctx, void *stream, uint64_t *fence_out)
+{
+    if (!ctx || !fence_out)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->fence_mu);
+    hipEvent_t ev;
+    if (!ctx->fence_pool.empty()) {
+        ev = ctx->fence_pool.back();
+        ctx->fence_pool.pop_back();
+    } else {
+        ZCHECK(ctx, hipSetDevice(ctx->device));
+        ZCHECK(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    hipError_t e = hipEventRecord(ev, (hipStream_t) stream);
+    if (e != hipSuccess) {
+        ctx->fence_pool.push_back(ev);
+        ZCHECK(ctx, e);
+    }
+    ctx->fences.emplace_back(++ctx->fence_ctr, ev);
+    *fence_out = ctx->fence_ctr;
+    return 0;
+}
+
+// 1 reached (and released), 0 pending, <0 error; `block` waits for it
+static int fence_check(zmqg_ctx *ctx, uint64_t fence, bool block)
+{
+    if (!ctx || fence == 0)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->fence_mu);
+    if (fence > ctx->fence_ctr)
+        return -EINVAL;
+    for (size_t i = 0; i < ctx->fences.size(); ++i) {
+        if (ctx->fences[i].first != fence)
+            continue;
+        hipEvent_t ev = ctx->fences[i].second;
+        hipError_t e = block ? hipEventSynchronize(ev) : hipEventQuery(ev);
+        if (e == hipErrorNotReady)
+            return 0;
+        ZCHECK(ctx, e);
+        ctx->fences.erase(ctx->fences.begin() + (long) i);
+        ctx->fence_pool.push_back(ev);
+        return 1;
+    }
+    return 1; // released earlier
+}
+
+int zmqg_fence_query(zmqg_ctx *ctx, uint64_t fence)
+{
+    return fence_check(ctx, fence, false);
+}
+
+int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence)
+{
+    const int rc = fence_check(ctx, fence, true);
+    return rc < 0 ? rc : 0;
 }
 
 } // extern "C"

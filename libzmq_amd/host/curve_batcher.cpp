@@ -1,0 +1,321 @@
+// curve_batcher.cpp -- see curve_batcher.hpp.
+#include "curve_batcher.hpp"
+
+#include <errno.h>
+#include <string.h>
+
+namespace zmqg
+{
+namespace
+{
+size_t align256 (size_t x)
+{
+    return (x + 255) & ~(size_t) 255;
+}
+
+//  largest wire growth over the payload: "\x07MESSAGE" + nonce + tag + the
+//  flags byte + up to 10 bytes of a downgraded SUBSCRIBE/CANCEL prefix
+//  (src/curve_mechanism_base.cpp:113-128, 169)
+const size_t max_wire_growth = 8 + 8 + 16 + 1 + 10;
+}
+
+curve_batcher_t::curve_batcher_t (zmqg_ctx *ctx_,
+                                  curve_sink_t *sink_,
+                                  const config_t &config_,
+                                  void *stream_) :
+    _ctx (ctx_),
+    _sink (sink_),
+    _config (config_),
+    _stream (stream_),
+    _out_cap (0)
+{
+    _open[0] = _open[1] = NULL;
+}
+
+curve_batcher_t::~curve_batcher_t ()
+{
+    //  nothing may still be reading or writing a slot when it is freed
+    for (size_t i = 0; i < _flight.size (); ++i)
+        zmqg_fence_wait (_ctx, _flight[i]->fence);
+    for (size_t i = 0; i < _slots.size (); ++i)
+        if (_slots[i].base)
+            zmqg_host_free (_ctx, _slots[i].base);
+}
+
+int curve_batcher_t::init ()
+{
+    if (!_ctx || !_sink || _config.slots < 2 || _config.slot_msgs == 0
+        || _config.slot_bytes == 0 || !_slots.empty ()) {
+        errno = EINVAL;
+        return -1;
+    }
+    if (!_stream && zmqg_ctx_stream (_ctx, &_stream) != 0) {
+        errno = EINVAL;
+        return -1;
+    }
+    const size_t m = _config.slot_msgs;
+    _out_cap = _config.slot_bytes + max_wire_growth * m;
+    const size_t o_sid = 0, o_nonce = align256 (o_sid + 4 * m),
+                 o_flags = align256 (o_nonce + 8 * m),
+                 o_in_off = align256 (o_flags + m),
+                 o_len = align256 (o_in_off + 8 * m),
+                 o_out_off = align256 (o_len + 4 * m),
+                 o_flags_out = align256 (o_out_off + 8 * m),
+                 o_status = align256 (o_flags_out + m),
+                 o_in = align256 (o_status + 4 * m),
+                 o_out = align256 (o_in + _config.slot_bytes),
+                 total = align256 (o_out + _out_cap);
+    _slots.resize (_config.slots);
+    for (size_t i = 0; i < _slots.size (); ++i) {
+        slot_t &s = _slots[i];
+        void *p = NULL;
+        const int rc = zmqg_host_alloc (_ctx, total, &p);
+        if (rc != 0) {
+            errno = -rc;
+            return -1;
+        }
+        uint8_t *b = static_cast<uint8_t *> (p);
+        s.base = b;
+        s.sid = reinterpret_cast<uint32_t *> (b + o_sid);
+        s.nonce = reinterpret_cast<uint64_t *> (b + o_nonce);
+        s.flags = b + o_flags;
+        s.in_off = reinterpret_cast<uint64_t *> (b + o_in_off);
+        s.len = reinterpret_cast<uint32_t *> (b + o_len);
+        s.out_off = reinterpret_cast<uint64_t *> (b + o_out_off);
+        s.flags_out = b + o_flags_out;
+        s.status = reinterpret_cast<int32_t *> (b + o_status);
+        s.in = b + o_in;
+        s.out = b + o_out;
+        s.tags.resize (m);
+        s.kind = encode_kind;
+        s.n = s.in_used = s.out_used = 0;
+        s.fence = 0;
+        _free.push_back (&s);
+    }
+    return 0;
+}
+
+int curve_batcher_t::wait_oldest ()
+{
+    slot_t *s = _flight.front ();
+    const int rc = zmqg_fence_wait (_ctx, s->fence);
+    if (rc != 0) {
+        errno = -rc;
+        return -1;
+    }
+    _flight.pop_front ();
+    return deliver (s);
+}
+
+//  Make _open[kind_] a slot with room for one more message of the given
+//  input / output bytes, launching the current one when it is full.
+int curve_batcher_t::open_slot (kind_t kind_, size_t in_need_, size_t out_need_)
+{
+    if (in_need_ > _config.slot_bytes || out_need_ > _out_cap) {
+        errno = EMSGSIZE;
+        return -1;
+    }
+    slot_t *s = _open[kind_];
+    if (s
+        && (s->n == _config.slot_msgs
+            || s->in_used + in_need_ > _config.slot_bytes
+            || s->out_used + out_need_ > _out_cap)) {
+        _open[kind_] = NULL;
+        if (launch (s) != 0)
+            return -1;
+        s = NULL;
+    }
+    if (!s) {
+        while (_free.empty ()) {
+            if (_flight.empty ()) {
+                errno = EAGAIN;
+                return -1;
+            }
+            if (wait_oldest () < 0)
+                return -1;
+        }
+        s = _free.back ();
+        _free.pop_back ();
+        s->kind = kind_;
+        s->n = s->in_used = s->out_used = 0;
+        _open[kind_] = s;
+    }
+    return 0;
+}
+
+int curve_batcher_t::submit_encode (curve_encoding_gpu_t *conn_,
+                                    const uint8_t *data_,
+                                    size_t size_,
+                                    uint8_t msg_flags_,
+                                    uint64_t tag_)
+{
+    if (_slots.empty () || !conn_ || conn_->_ctx != _ctx
+        || (size_ && !data_) || size_ > 0xffffffffu) {
+        errno = EINVAL;
+        return -1;
+    }
+    if (conn_->sync_session () != 0) {
+        errno = EIO;
+        return -1;
+    }
+    const size_t wire = static_cast<size_t> (
+      zmqg_wire_size (msg_flags_, conn_->_downgrade_sub ? 1 : 0, size_));
+    if (open_slot (encode_kind, size_, wire) != 0)
+        return -1;
+    slot_t *s = _open[encode_kind];
+    const size_t i = s->n++;
+    s->sid[i] = conn_->_sid;
+    s->nonce[i] = conn_->get_and_inc_nonce (); // src/curve_mechanism_base.cpp:114-116
+    s->flags[i] = msg_flags_;
+    s->in_off[i] = s->in_used;
+    s->len[i] = static_cast<uint32_t> (size_);
+    s->out_off[i] = s->out_used;
+    s->tags[i] = tag_;
+    if (size_)
+        memcpy (s->in + s->in_used, data_, size_);
+    s->in_used += size_;
+    s->out_used += wire;
+    return 0;
+}
+
+int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
+                                    const uint8_t *wire_,
+                                    size_t size_,
+                                    uint64_t tag_)
+{
+    if (_slots.empty () || !conn_ || conn_->_ctx != _ctx
+        || (size_ && !wire_) || size_ > 0xffffffffu) {
+        errno = EINVAL;
+        return -1;
+    }
+    if (conn_->sync_session () != 0) {
+        errno = EIO;
+        return -1;
+    }
+    const size_t plen = size_ >= 33 ? size_ - 33 : 0;
+    if (open_slot (decode_kind, size_, plen) != 0)
+        return -1;
+    slot_t *s = _open[decode_kind];
+    const size_t i = s->n++;
+    s->sid[i] = conn_->_sid;
+    s->in_off[i] = s->in_used;
+    s->len[i] = static_cast<uint32_t> (size_);
+    s->out_off[i] = s->out_used;
+    s->tags[i] = tag_;
+    if (size_)
+        memcpy (s->in + s->in_used, wire_, size_);
+    s->in_used += size_;
+    s->out_used += plen;
+    return 0;
+}
+
+int curve_batcher_t::launch (slot_t *s)
+{
+    int rc;
+    if (s->kind == encode_kind)
+        rc = zmqg_encode_batch (_ctx, s->n, s->sid, s->nonce, s->flags,
+                                s->in_off, s->len, s->in, s->out_off, s->out,
+                                _stream);
+    else
+        rc = zmqg_decode_batch (_ctx, s->n, s->sid, s->in_off, s->len, s->in,
+                                s->out_off, s->out, s->flags_out, s->status,
+                                _stream);
+    if (rc == 0)
+        rc = zmqg_fence_record (_ctx, _stream, &s->fence);
+    if (rc != 0) {
+        //  the slot's messages are lost with the device; keep the slot
+        _free.push_back (s);
+        errno = -rc;
+        return -1;
+    }
+    _flight.push_back (s);
+    return 0;
+}
+
+int curve_batcher_t::deliver (slot_t *s)
+{
+    const int n = static_cast<int> (s->n);
+    if (s->kind == encode_kind) {
+        for (size_t i = 0; i < s->n; ++i) {
+            const uint64_t end = i + 1 < s->n ? s->out_off[i + 1] : s->out_used;
+            _sink->on_encoded (s->tags[i], s->out + s->out_off[i],
+                               static_cast<size_t> (end - s->out_off[i]));
+        }
+    } else {
+        for (size_t i = 0; i < s->n; ++i) {
+            if (s->status[i] == 0)
+                _sink->on_decoded (s->tags[i], 0, s->out + s->out_off[i],
+                                   s->len[i] - 33u, s->flags_out[i]);
+            else
+                _sink->on_decoded (s->tags[i], s->status[i], NULL, 0, 0);
+        }
+    }
+    s->n = 0;
+    _free.push_back (s);
+    return n;
+}
+
+int curve_batcher_t::flush ()
+{
+    //  decode first: received frames usually gate the replies encoded next
+    const kind_t order[2] = {decode_kind, encode_kind};
+    for (int k = 0; k < 2; ++k) {
+        slot_t *s = _open[order[k]];
+        if (s && s->n) {
+            _open[order[k]] = NULL;
+            if (launch (s) != 0)
+                return -1;
+        }
+    }
+    return 0;
+}
+
+int curve_batcher_t::poll ()
+{
+    int delivered = 0;
+    while (!_flight.empty ()) {
+        const int rc = zmqg_fence_query (_ctx, _flight.front ()->fence);
+        if (rc < 0) {
+            errno = -rc;
+            return -1;
+        }
+        if (rc == 0)
+            break;
+        slot_t *s = _flight.front ();
+        _flight.pop_front ();
+        delivered += deliver (s);
+    }
+    return delivered;
+}
+
+int curve_batcher_t::drain ()
+{
+    if (flush () != 0)
+        return -1;
+    int delivered = 0;
+    while (!_flight.empty ()) {
+        const int rc = wait_oldest ();
+        if (rc < 0)
+            return -1;
+        delivered += rc;
+    }
+    return delivered;
+}
+
+size_t curve_batcher_t::queued () const
+{
+    size_t n = 0;
+    for (int k = 0; k < 2; ++k)
+        if (_open[k])
+            n += _open[k]->n;
+    return n;
+}
+
+size_t curve_batcher_t::in_flight () const
+{
+    size_t n = 0;
+    for (size_t i = 0; i < _flight.size (); ++i)
+        n += _flight[i]->n;
+    return n;
+}
+}

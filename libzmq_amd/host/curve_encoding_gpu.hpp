@@ -89,6 +89,8 @@ class curve_encoding_gpu_t
     nonce_t get_peer_nonce () const;
 
   private:
+    friend class curve_batcher_t;
+
     //  installs the session on the device when the precom buffer changed
     int sync_session ();
 

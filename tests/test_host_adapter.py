@@ -33,3 +33,65 @@ def test_adapter_roundtrips_on_gpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr + r.stdout
     assert r.stdout.strip() == "OK 7"
+
+
+def build_batcher_test(out_dir):
+    exe = os.path.join(out_dir, "test_curve_batcher")
+    cmd = ["g++", "-O2", "-std=c++11", "-Wall", "-Werror", "-o", exe,
+           os.path.join(ROOT, "tests", "host", "test_curve_batcher.cpp"),
+           os.path.join(ROOT, "libzmq_amd", "host", "curve_batcher.cpp"),
+           os.path.join(ROOT, "libzmq_amd", "host", "curve_encoding_gpu.cpp"),
+           "-L" + LIB_DIR, "-lzmqg_curve", "-Wl,-rpath," + LIB_DIR,
+           "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib"]
+    subprocess.check_call(cmd)
+    return exe
+
+
+def test_batcher_compiles_and_links(tmp_path):
+    assert os.path.exists(build_batcher_test(str(tmp_path)))
+
+
+def _read_batcher_records(path):
+    import numpy as np
+    raw = open(path, "rb").read()
+    n_conn, n_msgs = np.frombuffer(raw[:8], np.uint32)
+    p = 8
+    precoms = [raw[p + 32 * c:p + 32 * (c + 1)] for c in range(n_conn)]
+    p += 32 * n_conn
+    downgrade = list(raw[p:p + n_conn])
+    p += n_conn
+    recs = []
+    for _ in range(n_msgs):
+        conn, flags, plen, wlen = np.frombuffer(raw[p:p + 16], np.uint32)
+        p += 16
+        payload = raw[p:p + plen]
+        p += plen
+        wire = raw[p:p + wlen]
+        p += wlen
+        recs.append((int(conn), int(flags), payload, wire))
+    assert p == len(raw)
+    return precoms, downgrade, recs
+
+
+@pytest.mark.gpu
+def test_batcher_matches_per_message_path_and_oracle(tmp_path):
+    """The async batcher on a GPU (its own checks against the n = 1 path),
+    then every frame it encoded against the CPU oracle, one by one."""
+    import numpy as np
+    from oracle import oracle as O
+    exe = build_batcher_test(str(tmp_path))
+    dump = os.path.join(str(tmp_path), "records.bin")
+    r = subprocess.run([exe, dump], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert r.stdout.startswith("OK ")
+    precoms, downgrade, recs = _read_batcher_records(dump)
+    sessions = np.concatenate([O.make_sessions([p], downgrade_sub=bool(d)) for p, d in zip(precoms, downgrade)])
+    checked = 0
+    for conn, flags, payload, wire in recs:
+        nonce = int.from_bytes(wire[8:16], "big")
+        inp = np.frombuffer(payload, np.uint8) if payload else np.zeros(1, np.uint8)
+        ref = O.encode_batch(sessions, [conn], [nonce], [flags], [0], [len(payload)], inp, [0], len(wire))
+        assert O.wire_size(flags, downgrade[conn], len(payload)) == len(wire)
+        assert ref.tobytes() == wire
+        checked += 1
+    assert checked == len(recs) > 1000
