@@ -165,6 +165,23 @@ int zmqg_fence_record(zmqg_ctx *ctx, void *stream, uint64_t *fence_out);
 int zmqg_fence_query(zmqg_ctx *ctx, uint64_t fence);
 int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
 
+/* Batched Z85 key codec: zmq_z85_encode /
+ * zmq_z85_decode (src/zmq_utils.cpp:100-180, include/zmq.h:537-540) over n
+ * independent items, one per thread.  Item i: input bytes
+ * in[in_off[i] .. +len[i]), output at out[out_off[i]]; status_out[i] = 0 or
+ * EINVAL where the reference returns NULL with errno EINVAL.
+ *   encode: len % 4 == 0, writes len * 5 / 4 characters and a NUL.
+ *   decode: len = strlen of the string (>= 5, multiple of 5), writes
+ *     len * 4 / 5 bytes; an invalid character or a group above 0xffffffff
+ *     fails the item after the groups before it were written, as the
+ *     reference's loop does.
+ * Pointers as for the batch calls (device or device-accessible host memory);
+ * asynchronous on `stream`. */
+int zmqg_z85_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
+                          const uint64_t *out_off, char *out, int32_t *status_out, void *stream);
+int zmqg_z85_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint64_t *in_off, const uint32_t *len, const char *in,
+                          const uint64_t *out_off, uint8_t *out, int32_t *status_out, void *stream);
+
 /* Profiling hooks (off by default).  When enabled, the ctx records a HIP
  * event pair on the batch's stream around each of its kernels of one kind:
  *   ZMQG_PROF_ENCODE_MAIN / ZMQG_PROF_DECODE_MAIN  the frame kernel alone

@@ -43,6 +43,7 @@
 #include "../../include/zmqg_curve.h"
 #include "curve_device.hpp"
 #include "curve_frames.hpp"
+#include "curve_z85.hpp"
 
 #ifndef ZMQG_ABLATE
 #define ZMQG_ABLATE 0
@@ -1752,6 +1753,38 @@ int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     memcpy(out, h + o_out, out_bytes);
     memcpy(flags_out, h + o_fl, n);
     memcpy(status_out, h + o_st, 4 * n);
+    return 0;
+}
+
+int zmqg_z85_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
+                          const uint64_t *out_off, char *out, int32_t *status_out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!in_off || !len || !in || !out_off || !out || !status_out)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_z85_encode, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, (hipStream_t) stream,
+                       (uint32_t) n, in_off, len, in, out_off, out, status_out);
+    ZCHECK(ctx, hipGetLastError());
+    return 0;
+}
+
+int zmqg_z85_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint64_t *in_off, const uint32_t *len, const char *in,
+                          const uint64_t *out_off, uint8_t *out, int32_t *status_out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!in_off || !len || !in || !out_off || !out || !status_out)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_z85_decode, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, (hipStream_t) stream,
+                       (uint32_t) n, in_off, len, in, out_off, out, status_out);
+    ZCHECK(ctx, hipGetLastError());
     return 0;
 }
 

@@ -56,6 +56,14 @@ _lib.zmqg_encode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_encode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _U64, _P, _P, _U64]
 _lib.zmqg_decode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _U64, _P, _P, _U64, _P, _P]
+_lib.zmqg_z85_encode_batch.argtypes = [_P, _U64] + [_P] * 7
+_lib.zmqg_z85_decode_batch.argtypes = [_P, _U64] + [_P] * 7
+_lib.zmqg_host_alloc.argtypes = [_P, _U64, ctypes.POINTER(_P)]
+_lib.zmqg_host_free.argtypes = [_P, _P]
+_lib.zmqg_ctx_stream.argtypes = [_P, ctypes.POINTER(_P)]
+_lib.zmqg_fence_record.argtypes = [_P, _P, ctypes.POINTER(_U64)]
+_lib.zmqg_fence_query.argtypes = [_P, _U64]
+_lib.zmqg_fence_wait.argtypes = [_P, _U64]
 _lib.zmqg_ctx_set_profiling.argtypes = [_P, ctypes.c_int]
 _lib.zmqg_ctx_get_profile.argtypes = [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
 _lib.zmqg_last_error.argtypes = [_P]
@@ -166,6 +174,19 @@ class CurveContext:
         self._check(_lib.zmqg_decode_batch(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
                                            _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
                                            _stream_handle(stream)), "zmqg_decode_batch")
+
+    # ---- batched Z85 (zmq_z85_encode / zmq_z85_decode), device tensors ----
+    def z85_encode_batch(self, in_off, length, inp, out_off, out, status_out, stream=None):
+        n = int(in_off.numel())
+        self._check(_lib.zmqg_z85_encode_batch(self._ctx, n, _ptr(in_off), _ptr(length), _ptr(inp), _ptr(out_off),
+                                               _ptr(out), _ptr(status_out), _stream_handle(stream)),
+                    "zmqg_z85_encode_batch")
+
+    def z85_decode_batch(self, in_off, length, inp, out_off, out, status_out, stream=None):
+        n = int(in_off.numel())
+        self._check(_lib.zmqg_z85_decode_batch(self._ctx, n, _ptr(in_off), _ptr(length), _ptr(inp), _ptr(out_off),
+                                               _ptr(out), _ptr(status_out), _stream_handle(stream)),
+                    "zmqg_z85_decode_batch")
 
     # ---- host-memory batches (numpy), staged through pinned buffers ----
     def encode_host(self, sid, nonce, flags, in_off, length, inp, out_off, out_size):

@@ -45,6 +45,8 @@ def lib():
         L.oracle_decode_batch.argtypes = [_P, _P, _U64] + [_P] * 8
         L.oracle_bench_roundtrip.argtypes = [ctypes.c_int, ctypes.c_uint32, _P, _U64] + [_P] * 10
         L.oracle_bench_roundtrip.restype = ctypes.c_double
+        L.oracle_z85_encode.argtypes = [_P, _P, _U64]
+        L.oracle_z85_decode.argtypes = [_P, _P, _U64]
         assert L.oracle_session_size() == 68
         _lib = L
     return _lib
@@ -165,3 +167,22 @@ def bench_roundtrip(use_sodium, nthreads, sessions, sid, nonce, flags, in_off, l
     if secs < 0:
         return None, 0
     return secs, ok.value
+
+
+def z85_encode(data):
+    """zmq_z85_encode (src/zmq_utils.cpp:100-124): the string, or None (EINVAL)."""
+    data = bytes(data)
+    out = ctypes.create_string_buffer(len(data) * 5 // 4 + 1)
+    if lib().oracle_z85_encode(out, _buf(data), len(data)) != 0:
+        return None
+    return out.raw[:len(data) * 5 // 4]
+
+
+def z85_decode(string, fill=0):
+    """zmq_z85_decode (src/zmq_utils.cpp:131-180) of `string` (bytes, its
+    length standing for strlen): (rc, out) with rc 0 or 22 (EINVAL) and out the
+    len*4//5-byte destination, pre-filled with `fill`, as the call left it."""
+    string = bytes(string)
+    out = ctypes.create_string_buffer(bytes([fill]) * max(len(string) * 4 // 5, 1), max(len(string) * 4 // 5, 1))
+    rc = lib().oracle_z85_decode(out, _buf(string), len(string))
+    return rc, out.raw[:len(string) * 4 // 5]

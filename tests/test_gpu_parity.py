@@ -21,19 +21,6 @@ GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "curve
 H = bytes.fromhex
 
 
-@pytest.fixture(scope="module")
-def torch_cuda():
-    import torch
-    assert torch.cuda.is_available(), "GPU tests need a GPU"
-    return torch
-
-
-@pytest.fixture(scope="module")
-def C():
-    from libzmq_amd import curve
-    return curve
-
-
 def dev(torch, a):
     a = np.ascontiguousarray(a)
     if a.dtype == np.uint64:
