@@ -165,6 +165,49 @@ int zmqg_fence_record(zmqg_ctx *ctx, void *stream, uint64_t *fence_out);
 int zmqg_fence_query(zmqg_ctx *ctx, uint64_t fence);
 int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
 
+/* ZMTP framing on the device.
+ *
+ * zmqg_encode_zmtp: zmqg_encode_batch plus the engine's ZMTP encoder
+ * (src/v3_1_encoder.cpp:23-60) in one call: the n encoded MESSAGE commands
+ * are laid out back to back in `out` as ZMTP frames -- flags (0, or LARGE
+ * when the body exceeds 255 bytes; the boxed msg_t carries no MORE/COMMAND,
+ * src/curve_mechanism_base.cpp:166-177), size (1 byte, or 8 bytes big
+ * endian), body -- ready to be written to the socket.  frame_off[0..n]
+ * (device-accessible, n + 1 entries) receives each frame's offset and the
+ * total in frame_off[n]; offsets are computed on the device.  Asynchronous.
+ *
+ * zmqg_decode_zmtp: the engine's ZMTP decoder (src/v2_decoder.cpp:35-140)
+ * and curve_mechanism_base_t::decode over a received byte stream of one
+ * connection (session sid), on the device.  Frames are found from offset 0;
+ * up to max_frames of them are decoded: frame i's body is
+ * in[frame_in_off[i] .. +frame_len[i]), its payload is written at
+ * out[out_off[i]] and flags_out / status_out are as for zmqg_decode_batch,
+ * with the ZMTP frame's MORE / COMMAND bits ORed into flags_out of a
+ * decoded frame (msg_t::set_flags ORs, src/msg.cpp:433-436).  result:
+ * frames returned, bytes of `in` they cover (an incomplete last frame is
+ * left for the next call), payload bytes written, and error = EMSGSIZE when
+ * a frame's size exceeds max_msg_size (>= 0; -1 = no limit) or 2^32 - 1,
+ * where the reference decoder fails (src/v2_decoder.cpp:74-84): the frames
+ * before it are returned.  A complete frame that is not a MESSAGE command
+ * is returned as the last frame, with the status the mechanism gives it;
+ * the reference's engine stops at the first failing frame, and so should
+ * the caller.  Arrays hold max_frames entries; `out` at least in_bytes.
+ * Returns after the stream has synchronised.  in_bytes < 2^31. */
+typedef struct zmqg_zmtp_result {
+    uint64_t frames;
+    uint64_t consumed;
+    uint64_t out_bytes;
+    int32_t error;
+    int32_t pad;
+} zmqg_zmtp_result;
+int zmqg_encode_zmtp(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                     const uint64_t *in_off, const uint32_t *len, const uint8_t *in, uint8_t *out,
+                     uint64_t *frame_off, void *stream);
+int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
+                     uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
+                     uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result,
+                     void *stream);
+
 /* Batched Z85 key codec: zmq_z85_encode /
  * zmq_z85_decode (src/zmq_utils.cpp:100-180, include/zmq.h:537-540) over n
  * independent items, one per thread.  Item i: input bytes

@@ -44,6 +44,7 @@
 #include "curve_device.hpp"
 #include "curve_frames.hpp"
 #include "curve_z85.hpp"
+#include "curve_zmtp.hpp"
 
 #ifndef ZMQG_ABLATE
 #define ZMQG_ABLATE 0
@@ -144,6 +145,30 @@ struct Workspace {
 
 } // namespace
 
+namespace {
+// device buffers of the ZMTP framing calls
+struct ZmtpWs {
+    uint64_t n_cap = 0;                   // send side: frames
+    uint64_t *F = nullptr;                // [n_cap + 1] frame bytes
+    uint64_t *wire_off = nullptr;         // [n_cap] body offsets
+    uint64_t c_cap = 0;                   // receive side: candidates
+    uint64_t f_cap = 0;                   // receive side: frames
+    uint64_t *cand = nullptr;             // [c_cap]
+    uint64_t *bad = nullptr;              // [c_cap]
+    uint64_t *cand0 = nullptr;            // [c_cap] candidates as found (unordered)
+    uint64_t *run = nullptr;              // [2 c_cap]
+    uint64_t *runpre = nullptr;           // [c_cap]
+    uint64_t *psize = nullptr;            // [c_cap + 1]
+    uint64_t *poff = nullptr;             // [c_cap + 1]
+    uint32_t *sid_fill = nullptr;         // [c_cap]
+    uint8_t *fflags = nullptr;            // [c_cap]
+    unsigned long long *counts = nullptr; // [2] candidates, unlinked candidates
+    ZmtpWalk *walk = nullptr;
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+};
+} // namespace
+
 struct zmqg_ctx {
     int device = 0;
     int cus = 256; // compute units of the device (one persistent body workgroup each)
@@ -152,6 +177,7 @@ struct zmqg_ctx {
     DevSession *sessions = nullptr;
     unsigned long long *peer = nullptr; // [max_sessions]
     Workspace ws;
+    ZmtpWs zw;
     // host staging for the *_host entry points
     uint8_t *pin = nullptr;
     size_t pin_bytes = 0;
@@ -1390,6 +1416,14 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     for (void *p : ptrs)
         if (p)
             (void) hipFree(p);
+    {
+        ZmtpWs &z = ctx->zw;
+        void *zp[] = {z.F, z.wire_off, z.cand, z.bad, z.cand0, z.run, z.runpre, z.psize, z.poff, z.sid_fill, z.fflags,
+                      z.counts, z.walk, z.temp};
+        for (void *p : zp)
+            if (p)
+                (void) hipFree(p);
+    }
     if (ctx->pin)
         (void) hipHostFree(ctx->pin);
     if (ctx->own_stream)
@@ -1753,6 +1787,175 @@ int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     memcpy(out, h + o_out, out_bytes);
     memcpy(flags_out, h + o_fl, n);
     memcpy(status_out, h + o_st, 4 * n);
+    return 0;
+}
+
+static int zmtp_temp(zmqg_ctx *ctx, size_t need)
+{
+    ZmtpWs &z = ctx->zw;
+    if (need <= z.temp_bytes)
+        return 0;
+    size_t cap = z.temp_bytes ? z.temp_bytes : 4096;
+    while (cap < need)
+        cap *= 2;
+    if (z.temp)
+        ZCHECK(ctx, hipFree(z.temp));
+    z.temp = nullptr;
+    z.temp_bytes = 0;
+    ZCHECK(ctx, hipMalloc(&z.temp, cap));
+    z.temp_bytes = cap;
+    return 0;
+}
+
+int zmqg_encode_zmtp(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                     const uint64_t *in_off, const uint32_t *len, const uint8_t *in, uint8_t *out,
+                     uint64_t *frame_off, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (!frame_off)
+        return -EINVAL;
+    hipStream_t st = (hipStream_t) stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    if (n == 0)
+        return hipMemsetAsync(frame_off, 0, sizeof(uint64_t), st) == hipSuccess ? 0 : -EIO;
+    if (!sid || !nonce || !flags || !in_off || !len || !in || !out)
+        return -EINVAL;
+    ZmtpWs &z = ctx->zw;
+    int rc;
+    if (n > z.n_cap) {
+        uint64_t cap = z.n_cap ? z.n_cap : 1024;
+        while (cap < n)
+            cap *= 2;
+        if ((rc = grow(ctx, z.F, cap + 1)) || (rc = grow(ctx, z.wire_off, cap)))
+            return rc;
+        z.n_cap = cap;
+    }
+    size_t need = 0;
+    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.F, frame_off, (int) (n + 1), st));
+    if ((rc = zmtp_temp(ctx, need)))
+        return rc;
+    const unsigned g1 = (unsigned) ((n + 1 + 255) / 256), g0 = (unsigned) ((n + 255) / 256);
+    hipLaunchKernelGGL(k_zmtp_sizes, dim3(g1), dim3(256), 0, st, n, sid, flags, len, ctx->sessions,
+                       ctx->max_sessions, z.F);
+    ZCHECK(ctx, hipGetLastError());
+    size_t tb = z.temp_bytes;
+    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.F, frame_off, (int) (n + 1), st));
+    hipLaunchKernelGGL(k_zmtp_headers, dim3(g0), dim3(256), 0, st, n, frame_off, out, z.wire_off);
+    ZCHECK(ctx, hipGetLastError());
+    return zmqg_encode_batch(ctx, n, sid, nonce, flags, in_off, len, in, z.wire_off, out, stream);
+}
+
+int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
+                     uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
+                     uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result, void *stream)
+{
+    if (!ctx || !result || sid >= ctx->max_sessions || in_bytes > 0x7fffffffull || check_n(max_frames))
+        return -EINVAL;
+    memset(result, 0, sizeof *result);
+    if (in_bytes == 0 || max_frames == 0)
+        return 0;
+    if (!in || !frame_in_off || !frame_len || !out_off || !out || !flags_out || !status_out)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipStream_t st = (hipStream_t) stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    ZmtpWs &z = ctx->zw;
+    int rc;
+    // candidates: at most two per "\x07MESSAGE" occurrence, occurrences >= 8 bytes apart
+    const uint64_t ccap = in_bytes / 4 + 2;
+    if (ccap > z.c_cap) {
+        uint64_t cap = z.c_cap ? z.c_cap : 1024;
+        while (cap < ccap)
+            cap *= 2;
+        if ((rc = grow(ctx, z.cand, cap)) || (rc = grow(ctx, z.bad, cap)) || (rc = grow(ctx, z.cand0, cap)))
+            return rc;
+        z.c_cap = cap;
+    }
+    // frames (and chain runs, each holding a frame): at most max_frames
+    const uint64_t fcap = max_frames < ccap ? max_frames : ccap;
+    if (fcap > z.f_cap) {
+        uint64_t cap = z.f_cap ? z.f_cap : 1024;
+        while (cap < fcap)
+            cap *= 2;
+        if ((rc = grow(ctx, z.run, 2 * cap)) || (rc = grow(ctx, z.runpre, cap)) || (rc = grow(ctx, z.psize, cap + 1)) ||
+            (rc = grow(ctx, z.poff, cap + 1)) || (rc = grow(ctx, z.sid_fill, cap)) || (rc = grow(ctx, z.fflags, cap)))
+            return rc;
+        z.f_cap = cap;
+    }
+    if (!z.counts && (rc = grow(ctx, z.counts, 3)))
+        return rc;
+    if (!z.walk && (rc = grow(ctx, z.walk, 1)))
+        return rc;
+    hipcub::CountingInputIterator<uint64_t> pos(0);
+    // candidates (unordered), then sorted by offset
+    ZCHECK(ctx, hipMemsetAsync(z.counts, 0, 3 * sizeof(unsigned long long), st));
+    const uint64_t per_wg = 256ull * 16u * kZmtpScanIters;
+    hipLaunchKernelGGL(k_zmtp_scan, dim3((unsigned) ((in_bytes + per_wg - 1) / per_wg)), dim3(256), 0, st, in,
+                       in_bytes, max_msg_size, z.cand0, z.counts);
+    ZCHECK(ctx, hipGetLastError());
+    unsigned long long m = 0;
+    ZCHECK(ctx, hipMemcpyAsync(&m, z.counts, sizeof m, hipMemcpyDeviceToHost, st));
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    size_t need = 0, tb = 0;
+    if (m > 0) {
+        int bits = 1;
+        while (bits < 64 && (1ull << bits) < in_bytes)
+            ++bits;
+        ZCHECK(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, need, z.cand0, z.cand, (int) m, 0, bits, st));
+        if ((rc = zmtp_temp(ctx, need)))
+            return rc;
+        tb = z.temp_bytes;
+        ZCHECK(ctx, hipcub::DeviceRadixSort::SortKeys(z.temp, tb, z.cand0, z.cand, (int) m, 0, bits, st));
+    }
+    if (m > 0) {
+        const ZmtpIsUnlinked isu{in, in_bytes, z.cand, z.counts};
+        need = 0;
+        ZCHECK(ctx, hipcub::DeviceSelect::If(nullptr, need, pos, z.bad, z.counts + 1, (int) m, isu, st));
+        if ((rc = zmtp_temp(ctx, need)))
+            return rc;
+        tb = z.temp_bytes;
+        ZCHECK(ctx, hipcub::DeviceSelect::If(z.temp, tb, pos, z.bad, z.counts + 1, (int) m, isu, st));
+    } else {
+        ZCHECK(ctx, hipMemsetAsync(z.counts + 1, 0, sizeof(unsigned long long), st));
+    }
+    hipLaunchKernelGGL(k_zmtp_walk, dim3(1), dim3(64), 0, st, in, in_bytes, max_msg_size, max_frames, z.cand,
+                       z.counts, z.bad, z.counts + 1, z.run, z.runpre, z.walk);
+    ZCHECK(ctx, hipGetLastError());
+    const uint64_t mt = m ? m : 1;
+    hipLaunchKernelGGL(k_zmtp_frames, dim3((unsigned) ((mt + 255) / 256)), dim3(256), 0, st, in, in_bytes, z.cand,
+                       z.counts, z.run, z.runpre, z.walk, frame_in_off, frame_len, z.fflags);
+    ZCHECK(ctx, hipGetLastError());
+    ZmtpWalk w;
+    ZCHECK(ctx, hipMemcpyAsync(&w, z.walk, sizeof w, hipMemcpyDeviceToHost, st));
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    result->frames = w.frames;
+    result->consumed = w.consumed;
+    result->error = w.error;
+    const uint64_t nf = w.frames;
+    if (nf == 0)
+        return 0;
+    hipLaunchKernelGGL(k_zmtp_payload_sizes, dim3((unsigned) ((nf + 1 + 255) / 256)), dim3(256), 0, st, nf,
+                       frame_len, z.psize, z.sid_fill, sid);
+    ZCHECK(ctx, hipGetLastError());
+    need = 0;
+    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.psize, z.poff, (int) (nf + 1), st));
+    if ((rc = zmtp_temp(ctx, need)))
+        return rc;
+    tb = z.temp_bytes;
+    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.psize, z.poff, (int) (nf + 1), st));
+    ZCHECK(ctx, hipMemcpyAsync(out_off, z.poff, nf * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    rc = zmqg_decode_batch(ctx, nf, z.sid_fill, frame_in_off, frame_len, in, z.poff, out, flags_out, status_out,
+                           stream);
+    if (rc)
+        return rc;
+    hipLaunchKernelGGL(k_zmtp_flags, dim3((unsigned) ((nf + 255) / 256)), dim3(256), 0, st, nf, z.fflags,
+                       status_out, flags_out);
+    ZCHECK(ctx, hipGetLastError());
+    unsigned long long ob = 0;
+    ZCHECK(ctx, hipMemcpyAsync(&ob, z.poff + nf, sizeof ob, hipMemcpyDeviceToHost, st));
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    result->out_bytes = ob;
     return 0;
 }
 

@@ -56,6 +56,14 @@ _lib.zmqg_encode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_encode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _U64, _P, _P, _U64]
 _lib.zmqg_decode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _U64, _P, _P, _U64, _P, _P]
+class ZmtpResult(ctypes.Structure):  # zmqg_zmtp_result
+    _fields_ = [("frames", _U64), ("consumed", _U64), ("out_bytes", _U64), ("error", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
+
+
+_lib.zmqg_encode_zmtp.argtypes = [_P, _U64] + [_P] * 9
+_lib.zmqg_decode_zmtp.argtypes = [_P, _U32, _P, _U64, ctypes.c_int64, _U64] + [_P] * 6 + [ctypes.POINTER(ZmtpResult),
+                                                                                       _P]
 _lib.zmqg_z85_encode_batch.argtypes = [_P, _U64] + [_P] * 7
 _lib.zmqg_z85_decode_batch.argtypes = [_P, _U64] + [_P] * 7
 _lib.zmqg_host_alloc.argtypes = [_P, _U64, ctypes.POINTER(_P)]
@@ -174,6 +182,26 @@ class CurveContext:
         self._check(_lib.zmqg_decode_batch(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
                                            _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
                                            _stream_handle(stream)), "zmqg_decode_batch")
+
+    # ---- ZMTP framing on the device (device tensors) ----
+    def encode_zmtp(self, sid, nonce, flags, in_off, length, inp, out, frame_off, stream=None):
+        """Encode and frame n messages back to back in `out`; frame_off (n + 1
+        int64) receives the frame offsets and the total."""
+        n = int(sid.numel())
+        self._check(_lib.zmqg_encode_zmtp(self._ctx, n, _ptr(sid), _ptr(nonce), _ptr(flags), _ptr(in_off),
+                                          _ptr(length), _ptr(inp), _ptr(out), _ptr(frame_off),
+                                          _stream_handle(stream)), "zmqg_encode_zmtp")
+
+    def decode_zmtp(self, sid, inp, in_bytes, max_msg_size, max_frames, frame_in_off, frame_len, out_off, out,
+                    flags_out, status_out, stream=None):
+        """Parse and decode a received stream of one connection; returns
+        dict(frames, consumed, out_bytes, error)."""
+        r = ZmtpResult()
+        self._check(_lib.zmqg_decode_zmtp(self._ctx, sid, _ptr(inp), in_bytes, max_msg_size, max_frames,
+                                          _ptr(frame_in_off), _ptr(frame_len), _ptr(out_off), _ptr(out),
+                                          _ptr(flags_out), _ptr(status_out), ctypes.byref(r),
+                                          _stream_handle(stream)), "zmqg_decode_zmtp")
+        return dict(frames=r.frames, consumed=r.consumed, out_bytes=r.out_bytes, error=r.error)
 
     # ---- batched Z85 (zmq_z85_encode / zmq_z85_decode), device tensors ----
     def z85_encode_batch(self, in_off, length, inp, out_off, out, status_out, stream=None):

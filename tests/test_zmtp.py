@@ -1,0 +1,164 @@
+"""ZMTP framing on the device: zmqg_encode_zmtp /
+zmqg_decode_zmtp against oracle/zmtp_oracle.py (the reference's ZMTP encoder
+and decoder loop, src/v3_1_encoder.cpp:23-60, src/v2_decoder.cpp:35-140)
+combined with the CURVE oracle.  Cases follow the decoder's branches: short
+and LARGE sizes (the 255-byte boundary, LARGE with a small size), EMSGSIZE,
+incomplete header / body at the buffer end, a non-MESSAGE frame, planted
+"\\x07MESSAGE" signatures inside bodies, max_frames."""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import zmtp_oracle as Z
+from tests.helpers import random_batch, wire_layout
+
+
+def test_oracle_frame_boundary():
+    assert Z.frame(b"\x07MESSAGE" + bytes(247)) [:2] == b"\x00\xff"
+    f = Z.frame(b"\x07MESSAGE" + bytes(248))
+    assert f[0] == Z.LARGE and struct.unpack(">Q", f[1:9])[0] == 256
+
+
+def test_oracle_parse_branches():
+    body = b"\x07MESSAGE" + bytes(30)
+    s = Z.frame(body) + bytes([Z.LARGE]) + struct.pack(">Q", len(body)) + body  # LARGE with a small size
+    r = Z.parse(s)
+    assert [f[2] for f in r["frames"]] == [38, 38] and r["consumed"] == len(s) and r["error"] == 0
+    assert Z.parse(s[:-1])["consumed"] == 40  # incomplete body
+    assert Z.parse(s + b"\x02\x00\x00")["consumed"] == len(s)  # incomplete LARGE header
+    r = Z.parse(s, max_msg_size=37)
+    assert r["frames"] == [] and r["error"] == Z.EMSGSIZE
+    ping = Z.frame(b"\x04PING\x00\x00")
+    r = Z.parse(ping + s)
+    assert len(r["frames"]) == 1 and r["consumed"] == len(ping)  # the mechanism rejects it: stop
+    assert len(Z.parse(s, max_frames=1)["frames"]) == 1
+
+
+@pytest.mark.gpu
+def test_encode_zmtp_matches_oracle(torch_cuda, C):
+    torch = torch_cuda
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(2)
+    n, S = 1500, 4
+    precoms = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(S)]
+    downgrade = [False, True, False, False]
+    b = random_batch(rng, n, [0, 1, 100, 221, 222, 223, 250, 300, 1024, 5000, 70000], S,
+                     flag_choices=(0, 1, 2, 3, 12, 16))
+    ctx = C.CurveContext(0, S)
+    for s in range(S):
+        ctx.session_set(s, precoms[s], C.CLIENT_PREFIX, C.SERVER_PREFIX, downgrade[s])
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(dev)
+    wires = [O.wire_size(int(f), downgrade[int(s)], int(l)) for f, s, l in zip(b["flags"], b["sid"], b["lens"])]
+    total = sum(w + (9 if w > 255 else 2) for w in wires)
+    out = torch.full((total + 64,), 0xEE, dtype=torch.uint8, device=dev)
+    foff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    ctx.encode_zmtp(t(b["sid"], np.int32), t(b["nonce"], np.int64), t(b["flags"], np.uint8), t(b["in_off"], np.int64),
+                    t(b["lens"], np.int32), t(b["inp"], np.uint8), out, foff)
+    torch.cuda.synchronize()
+    got, fo = out.cpu().numpy(), foff.cpu().numpy()
+    assert int(fo[n]) == total and (got[total:] == 0xEE).all()
+    sessions = np.concatenate([O.make_sessions([p], downgrade_sub=d) for p, d in zip(precoms, downgrade)])
+    out_off, wl, wtotal = wire_layout(b["flags"], b["lens"], downgrade, b["sid"])
+    ref_wire = O.encode_batch(sessions, b["sid"], b["nonce"], b["flags"], b["in_off"], b["lens"], b["inp"], out_off,
+                              wtotal)
+    ref = b"".join(Z.frame(ref_wire[int(out_off[i]):int(out_off[i]) + int(wl[i])]) for i in range(n))
+    assert got[:total].tobytes() == ref
+    pos = 0
+    for i in range(n):
+        assert int(fo[i]) == pos
+        pos += int(wl[i]) + (9 if wl[i] > 255 else 2)
+
+
+def _stream_case(rng, case, precom, n=400):
+    """A received byte stream of one connection and the decoder settings."""
+    b = random_batch(rng, n, [0, 5, 100, 222, 223, 1024, 3000], 1, flag_choices=(0, 1, 2))
+    sessions = O.make_sessions([precom])
+    out_off, wl, wtotal = wire_layout(b["flags"], b["lens"], [False], b["sid"])
+    wire = O.encode_batch(sessions, b["sid"], b["nonce"], b["flags"], b["in_off"], b["lens"], b["inp"], out_off, wtotal)
+    bodies = [bytearray(wire[int(out_off[i]):int(out_off[i]) + int(wl[i])].tobytes()) for i in range(n)]
+    frames = []
+    max_msg, max_frames = -1, 1 << 20
+    for i, body in enumerate(bodies):
+        if case == "planted" and rng.random() < 0.2 and len(body) > 60:
+            # a frame-like header and the MESSAGE signature inside the ciphertext
+            k = int(rng.integers(33, len(body) - 20))
+            fake = bytes([0, int(rng.integers(8, 40))]) + b"\x07MESSAGE"
+            body[k:k + len(fake)] = fake
+        if case == "large_small" and rng.random() < 0.3 and len(body) <= 255:
+            frames.append(bytes([Z.LARGE]) + struct.pack(">Q", len(body)) + bytes(body))
+            continue
+        frames.append(Z.frame(body))
+    if case == "ping":
+        frames.insert(n // 2, Z.frame(b"\x04PING\x00\x00\x00"))
+    stream = b"".join(frames)
+    if case == "truncated":
+        stream = stream[:int(rng.integers(len(stream) // 2, len(stream) - 1))]
+    if case == "emsgsize":
+        max_msg = 2000
+    if case == "max_frames":
+        max_frames = 123
+    if case == "zmtp_flags":
+        # MORE / COMMAND bits on some frame headers (the decoder passes them on)
+        stream = bytearray(stream)
+        pos = 0
+        for f in frames:
+            if rng.random() < 0.3:
+                stream[pos] |= int(rng.choice([Z.MORE, Z.COMMAND, Z.MORE | Z.COMMAND]))
+            pos += len(f)
+        stream = bytes(stream)
+    return stream, max_msg, max_frames
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["clean", "truncated", "planted", "large_small", "ping", "emsgsize", "max_frames",
+                                  "zmtp_flags"])
+def test_decode_zmtp_matches_oracle(torch_cuda, C, case):
+    torch = torch_cuda
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(zlib.crc32(case.encode()))
+    precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    stream, max_msg, max_frames = _stream_case(rng, case, precom)
+    ref = Z.parse(stream, max_msg, max_frames if max_frames < (1 << 20) else None)
+    # CURVE decode of the frames the decoder produced, in order (peer nonce 2)
+    fr = ref["frames"]
+    nf = len(fr)
+    f_off = np.array([f[1] for f in fr], np.uint64)
+    f_len = np.array([f[2] for f in fr], np.uint32)
+    plen = np.maximum(f_len.astype(np.int64) - 33, 0)
+    p_off = np.concatenate([[0], np.cumsum(plen)[:-1]]).astype(np.uint64) if nf else np.zeros(0, np.uint64)
+    dec = O.make_sessions([precom], dec_prefix=O.CLIENT_PREFIX)
+    inp = np.frombuffer(stream, np.uint8)
+    pl, fl, st = O.decode_batch(dec, np.array([2], np.uint64), np.zeros(nf, np.uint32), f_off, f_len, inp, p_off,
+                                int(plen.sum()))
+    fl = np.array([int(fl[i]) | (Z.msg_flags(fr[i][0]) if st[i] == 0 else 0) for i in range(nf)], np.uint8)
+
+    ctx = C.CurveContext(0, 1)
+    ctx.session_set(0, precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+    cap = 1000
+    d_in = torch.from_numpy(inp.copy()).to(dev)
+    d_foff = torch.zeros(cap, dtype=torch.int64, device=dev)
+    d_flen = torch.zeros(cap, dtype=torch.int32, device=dev)
+    d_poff = torch.zeros(cap, dtype=torch.int64, device=dev)
+    d_out = torch.full((len(stream) + 1,), 0x77, dtype=torch.uint8, device=dev)
+    d_fl = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    d_st = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+    r = ctx.decode_zmtp(0, d_in, len(stream), max_msg, max_frames, d_foff, d_flen, d_poff, d_out, d_fl, d_st)
+    assert r["frames"] == nf and r["consumed"] == ref["consumed"] and r["error"] == ref["error"], (r, ref["consumed"])
+    assert r["out_bytes"] == int(plen.sum())
+    assert (d_foff[:nf].cpu().numpy().view(np.uint64) == f_off).all()
+    assert (d_flen[:nf].cpu().numpy().view(np.uint32) == f_len).all()
+    assert (d_poff[:nf].cpu().numpy().view(np.uint64) == p_off).all()
+    assert (d_st[:nf].cpu().numpy() == st).all()
+    assert (d_fl[:nf].cpu().numpy() == fl).all()
+    assert d_out[:int(plen.sum())].cpu().numpy().tobytes() == pl[:int(plen.sum())].tobytes()
+    if case in ("clean", "large_small", "zmtp_flags"):
+        assert (st == 0).all() and ref["consumed"] == len(stream)
+    if case == "planted":
+        assert (st == C.ERR_CRYPTOGRAPHIC).any() and ref["consumed"] == len(stream)
+    if case == "ping":
+        assert st[-1] != 0 and (st[:-1] == 0).all()
+    if case == "emsgsize":
+        assert ref["error"] == Z.EMSGSIZE
