@@ -208,6 +208,24 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
                      uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result,
                      void *stream);
 
+/* Handshake key derivation in batches, one
+ * 32-byte item per thread, items packed back to back:
+ *   zmqg_scalarmult_batch: crypto_scalarmult_curve25519(out, scalar, point)
+ *     (libsodium 1.0.18; RFC 7748 X25519): status -1 where the result is all
+ *     zero (a small-order point), else 0.  point == NULL: the base point, as
+ *     crypto_scalarmult_base for zmq_curve_public (src/zmq_utils.cpp:222-245);
+ *     status always 0.
+ *   zmqg_box_beforenm_batch: crypto_box_beforenm(k, pk, sk) =
+ *     HSalsa20(X25519(sk, pk), 0^16), the connection's precomputed key
+ *     (src/curve_client_tools.hpp:105, src/curve_server.cpp:382-383; the
+ *     reference asserts success): status -1 and k not written where the
+ *     scalar multiplication fails.
+ * Asynchronous on `stream`; pointers as for the batch calls. */
+int zmqg_scalarmult_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *scalar, const uint8_t *point, uint8_t *out,
+                          int32_t *status_out, void *stream);
+int zmqg_box_beforenm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *pk, const uint8_t *sk, uint8_t *k_out,
+                            int32_t *status_out, void *stream);
+
 /* Batched Z85 key codec: zmq_z85_encode /
  * zmq_z85_decode (src/zmq_utils.cpp:100-180, include/zmq.h:537-540) over n
  * independent items, one per thread.  Item i: input bytes

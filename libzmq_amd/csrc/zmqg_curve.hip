@@ -44,6 +44,7 @@
 #include "curve_device.hpp"
 #include "curve_frames.hpp"
 #include "curve_z85.hpp"
+#include "curve_x25519.hpp"
 #include "curve_zmtp.hpp"
 
 #ifndef ZMQG_ABLATE
@@ -1956,6 +1957,38 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
     ZCHECK(ctx, hipMemcpyAsync(&ob, z.poff + nf, sizeof ob, hipMemcpyDeviceToHost, st));
     ZCHECK(ctx, hipStreamSynchronize(st));
     result->out_bytes = ob;
+    return 0;
+}
+
+int zmqg_scalarmult_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *scalar, const uint8_t *point, uint8_t *out,
+                          int32_t *status_out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!scalar || !out || !status_out)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_scalarmult, dim3((unsigned) ((n + 63) / 64)), dim3(64), 0, (hipStream_t) stream,
+                       (uint32_t) n, scalar, point, out, status_out);
+    ZCHECK(ctx, hipGetLastError());
+    return 0;
+}
+
+int zmqg_box_beforenm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *pk, const uint8_t *sk, uint8_t *k_out,
+                            int32_t *status_out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!pk || !sk || !k_out || !status_out)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_beforenm, dim3((unsigned) ((n + 63) / 64)), dim3(64), 0, (hipStream_t) stream,
+                       (uint32_t) n, pk, sk, k_out, status_out);
+    ZCHECK(ctx, hipGetLastError());
     return 0;
 }
 

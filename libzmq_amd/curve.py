@@ -64,6 +64,8 @@ class ZmtpResult(ctypes.Structure):  # zmqg_zmtp_result
 _lib.zmqg_encode_zmtp.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_zmtp.argtypes = [_P, _U32, _P, _U64, ctypes.c_int64, _U64] + [_P] * 6 + [ctypes.POINTER(ZmtpResult),
                                                                                        _P]
+_lib.zmqg_scalarmult_batch.argtypes = [_P, _U64] + [_P] * 5
+_lib.zmqg_box_beforenm_batch.argtypes = [_P, _U64] + [_P] * 5
 _lib.zmqg_z85_encode_batch.argtypes = [_P, _U64] + [_P] * 7
 _lib.zmqg_z85_decode_batch.argtypes = [_P, _U64] + [_P] * 7
 _lib.zmqg_host_alloc.argtypes = [_P, _U64, ctypes.POINTER(_P)]
@@ -202,6 +204,19 @@ class CurveContext:
                                           _ptr(flags_out), _ptr(status_out), ctypes.byref(r),
                                           _stream_handle(stream)), "zmqg_decode_zmtp")
         return dict(frames=r.frames, consumed=r.consumed, out_bytes=r.out_bytes, error=r.error)
+
+    # ---- handshake key derivation (device tensors of n x 32 bytes) ----
+    def scalarmult_batch(self, scalar, point, out, status_out, stream=None):
+        """crypto_scalarmult_curve25519 per item; point None = the base point."""
+        n = int(status_out.numel())
+        self._check(_lib.zmqg_scalarmult_batch(self._ctx, n, _ptr(scalar), _ptr(point), _ptr(out), _ptr(status_out),
+                                               _stream_handle(stream)), "zmqg_scalarmult_batch")
+
+    def box_beforenm_batch(self, pk, sk, k_out, status_out, stream=None):
+        """crypto_box_beforenm(k, pk, sk) per item."""
+        n = int(status_out.numel())
+        self._check(_lib.zmqg_box_beforenm_batch(self._ctx, n, _ptr(pk), _ptr(sk), _ptr(k_out), _ptr(status_out),
+                                                 _stream_handle(stream)), "zmqg_box_beforenm_batch")
 
     # ---- batched Z85 (zmq_z85_encode / zmq_z85_decode), device tensors ----
     def z85_encode_batch(self, in_off, length, inp, out_off, out, status_out, stream=None):

@@ -45,6 +45,8 @@ def lib():
         L.oracle_decode_batch.argtypes = [_P, _P, _U64] + [_P] * 8
         L.oracle_bench_roundtrip.argtypes = [ctypes.c_int, ctypes.c_uint32, _P, _U64] + [_P] * 10
         L.oracle_bench_roundtrip.restype = ctypes.c_double
+        L.oracle_x25519.argtypes = [_P, _P, _P]
+        L.oracle_box_beforenm.argtypes = [_P, _P, _P]
         L.oracle_z85_encode.argtypes = [_P, _P, _U64]
         L.oracle_z85_decode.argtypes = [_P, _P, _U64]
         assert L.oracle_session_size() == 68
@@ -186,3 +188,17 @@ def z85_decode(string, fill=0):
     out = ctypes.create_string_buffer(bytes([fill]) * max(len(string) * 4 // 5, 1), max(len(string) * 4 // 5, 1))
     rc = lib().oracle_z85_decode(out, _buf(string), len(string))
     return rc, out.raw[:len(string) * 4 // 5]
+
+
+def x25519(scalar, point):
+    """crypto_scalarmult_curve25519 (libsodium 1.0.18 semantics): (rc, out)."""
+    out = ctypes.create_string_buffer(32)
+    rc = lib().oracle_x25519(out, _buf(bytes(scalar)), _buf(bytes(point)))
+    return rc, out.raw
+
+
+def box_beforenm(pk, sk):
+    """crypto_box_beforenm(k, pk, sk): (rc, k or None)."""
+    k = ctypes.create_string_buffer(32)
+    rc = lib().oracle_box_beforenm(k, _buf(bytes(pk)), _buf(bytes(sk)))
+    return rc, (k.raw if rc == 0 else None)
