@@ -126,13 +126,25 @@ __device__ __forceinline__ void frame_load_raw(uint64_t A, uint32_t w, uint32_t 
 }
 
 // Stream words of window w from the raw words (zero at and beyond S).
-__device__ __forceinline__ void frame_words(const uint32_t d[17], uint32_t v, uint32_t w, uint32_t S, uint32_t x[16])
+// The tail mask runs only when some lane of the wave is on its frame's last
+// window (a wave-uniform branch): if-converted, its 16 selects per word
+// would be paid on every window.
+__device__ __forceinline__ void mask_tail_wave(uint32_t x[16], uint32_t w, uint32_t S, bool act)
+{
+    if (__builtin_amdgcn_ballot_w64(act && S < 64u * w + 64u) != 0) {
+        if (S < 64u * w + 64u)
+            mask_tail(x, (int) (S - 64u * w));
+    }
+}
+
+__device__ __forceinline__ void frame_words(const uint32_t d[17], uint32_t v, uint32_t w, uint32_t S, uint32_t x[16],
+                                            bool mask, bool act)
 {
 #pragma unroll
     for (int k = 0; k < 16; ++k)
         x[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], v);
-    if (S < 64u * w + 64u)
-        mask_tail(x, (int) (S - 64u * w));
+    if (mask)
+        mask_tail_wave(x, w, S, act);
 }
 
 // Store output stream words y of window w >= 1 (stream byte 0 at B): the 16
@@ -509,7 +521,9 @@ __global__ __launch_bounds__(256) void k_frames(
         const bool act = w < nw;
         // the keystream first: it needs no input, so the wait for this
         // step's words (and, vmcnt being in order, for the previous step's
-        // stores issued after them) comes after ~1000 instructions of Salsa20
+        // stores issued after them) comes after ~1000 instructions of Salsa20.
+        // (Its counter-free first-round steps are loop-invariant: the
+        // compiler hoists them, so they are computed once per lane.)
         uint32_t ks[16];
         salsa20_block(ks, key, n0, n1, w, 0);
         uint32_t dc[17];
@@ -546,7 +560,7 @@ __global__ __launch_bounds__(256) void k_frames(
                 for (int k = 0; k < 16; ++k)
                     x[k] = dc[k];
             } else {
-                frame_words(dc, vin, w, S, x);
+                frame_words(dc, vin, w, S, x, DEC, act); // encode masks the ciphertext instead
             }
         }
         // r from keystream block 0 (lane 0 of the group) to the group
@@ -580,21 +594,21 @@ __global__ __launch_bounds__(256) void k_frames(
         // ciphertext words c (the Poly1305 input) and output words y
         uint32_t c[16], y[16];
         if (DEC) {
+            // y beyond S is never stored (frame_store and window 0's
+            // store_window are byte-exact), so only the MAC input is masked
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 c[k] = x[k];
                 y[k] = x[k] ^ ks[k];
             }
-            if (S < 64u * w + 64u)
-                mask_tail(y, (int) (S - 64u * w));
         } else {
 #pragma unroll
             for (int k = 0; k < 16; ++k)
-                y[k] = c[k] = x[k] ^ ks[k];
-            if (S < 64u * w + 64u) {
-                mask_tail(c, (int) (S - 64u * w));
-                mask_tail(y, (int) (S - 64u * w));
-            }
+                c[k] = x[k] ^ ks[k];
+            mask_tail_wave(c, w, S, act);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                y[k] = c[k];
         }
         if (w == 0) {
 #pragma unroll
@@ -704,11 +718,12 @@ __global__ __launch_bounds__(256) void k_frames(
         const uint32_t y15 = act ? y[15] : 0u;
         const uint32_t fromleft = (uint32_t) __shfl((int) y15, (int) (lane > 0 ? lane - 1 : 0));
         const uint32_t yprev = q == 0 ? ycarry : fromleft;
-        if (act && w > 0)
+        if (act && w > 0) {
             if (!(ZMQG_FRAMES_ABLATE & 2))
                 frame_store(B, w, S, y, yprev, w == L);
             else
                 *(GU32 *) (uintptr_t) (B + 64ull * w) = y[0] ^ y[5] ^ y[9] ^ y[15] ^ yprev;
+        }
         ycarry = (uint32_t) __shfl((int) y15, (int) (gbase + G - 1));
     }
     // H_q * r^(kb + 4(L-1-lastH)), plus U'_L (already in tot)
