@@ -1,0 +1,147 @@
+"""GPU parity at BASELINE.json's full per-GPU sizes (configs 4 and 5).
+
+At these sizes (4 GiB and 2 GiB of payload) the CPU oracle cannot check every
+byte in seconds, so each test combines
+  * size-independent properties over the whole batch, on the device: the
+    decode of the encoded batch returns every payload byte and flag, every
+    status is 0, and each session's peer nonce ends at its last nonce;
+  * bit-exact oracle checks of a seeded sample of frames (wire bytes and tag
+    of each sampled frame recomputed by oracle/curve_oracle.c).
+Inputs are generated on the device from a seed (torch Philox), descriptors as
+SURVEY.md section 8(d) specifies for the config.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(n_sessions, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(n_sessions)]
+
+
+def _contexts(C, keys):
+    enc = C.CurveContext(0, len(keys))
+    dec = C.CurveContext(0, len(keys))
+    for s, k in enumerate(keys):
+        enc.session_set(s, k, O.CLIENT_PREFIX, O.SERVER_PREFIX)
+        dec.session_set(s, k, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    return enc, dec
+
+
+def _check_sample(torch, keys, idx, sid, nonce, flags, P, payload, wire, W):
+    """Oracle encode of the sampled frames idx (sid, nonce, flags: theirs, in
+    sample order) == their wire bytes on the device."""
+    k = len(idx)
+    ti = torch.from_numpy(idx.astype(np.int64)).to("cuda")
+    pay = payload.view(-1, P)[ti].cpu().numpy().reshape(-1)
+    got = wire.view(-1, W)[ti].cpu().numpy().reshape(-1)
+    ref = O.encode_batch(O.make_sessions(keys), sid.astype(np.uint32), nonce.astype(np.uint64),
+                         flags.astype(np.uint8), np.arange(k, dtype=np.uint64) * P, np.full(k, P, np.uint32),
+                         pay, np.arange(k, dtype=np.uint64) * W, k * W)
+    assert np.array_equal(got, ref)
+
+
+def test_config4_full_size_flood(torch_cuda, C):
+    """Config 4 at the size of one GPU's whole batch: 16 Mi x 256 B frames over
+    1024 sessions (sid = i mod 1024), per-session sequential nonces from 3,
+    MORE on one frame in 16."""
+    torch = torch_cuda
+    n, P, ns = 16 << 20, 256, 1024
+    W = P + 33
+    keys = _keys(ns, 40)
+    enc, dec = _contexts(C, keys)
+    i = torch.arange(n, device="cuda", dtype=torch.int64)
+    sid = (i % ns).to(torch.int32)
+    nonce = 3 + i // ns
+    flags = (i % 16 == 15).to(torch.uint8)
+    in_off = i * P
+    lens = torch.full((n,), P, dtype=torch.int32, device="cuda")
+    out_off = i * W
+    g = torch.Generator(device="cuda")
+    g.manual_seed(41)
+    payload = torch.randint(0, 256, (n * P,), dtype=torch.uint8, device="cuda", generator=g)
+    wire = torch.zeros(n * W, dtype=torch.uint8, device="cuda")
+    enc.encode_batch(sid, nonce, flags, in_off, lens, payload, out_off, wire)
+    back = torch.zeros(n * P, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    wl = torch.full((n,), W, dtype=torch.int32, device="cuda")
+    dec.decode_batch(sid, out_off, wl, wire, in_off, back, fl, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert torch.equal(fl, flags)
+    assert torch.equal(back, payload)
+    last = 3 + (n // ns) - 1
+    for s in (0, 1, 511, 1023):
+        assert dec.get_peer_nonce(s) == last
+    rng = np.random.default_rng(42)
+    idx = np.sort(rng.choice(n, 4096, replace=False))
+    idx[:2] = [0, 1]
+    idx[-1] = n - 1
+    ii = idx.astype(np.int64)
+    _check_sample(torch, keys, idx, (ii % ns), 3 + ii // ns, (ii % 16 == 15), P, payload, wire, W)
+
+
+def test_config4_replay_of_a_flood_slice(torch_cuda, C):
+    """Re-decoding any frame of an accepted batch is a replay (nonce not above
+    the session's peer nonce): every frame is rejected with
+    ZMQ_PROTOCOL_ERROR_ZMTP_INVALID_SEQUENCE and its payload region zeroed."""
+    torch = torch_cuda
+    n, P, ns = 1 << 20, 256, 1024
+    W = P + 33
+    keys = _keys(ns, 43)
+    enc, dec = _contexts(C, keys)
+    i = torch.arange(n, device="cuda", dtype=torch.int64)
+    sid = (i % ns).to(torch.int32)
+    nonce = 3 + i // ns
+    flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    lens = torch.full((n,), P, dtype=torch.int32, device="cuda")
+    payload = torch.randint(0, 256, (n * P,), dtype=torch.uint8, device="cuda")
+    wire = torch.zeros(n * W, dtype=torch.uint8, device="cuda")
+    enc.encode_batch(sid, nonce, flags, i * P, lens, payload, i * W, wire)
+    wl = torch.full((n,), W, dtype=torch.int32, device="cuda")
+    back = torch.zeros(n * P, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    dec.decode_batch(sid, i * W, wl, wire, i * P, back, fl, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0 and torch.equal(back, payload)
+    back.fill_(0x5a)
+    dec.decode_batch(sid, i * W, wl, wire, i * P, back, fl, st)
+    torch.cuda.synchronize()
+    assert int((st != C.ERR_INVALID_SEQUENCE).sum()) == 0
+    assert int(back.count_nonzero()) == 0
+
+
+def test_config5_jumbo_per_gpu_share(torch_cuda, C):
+    """Config 5's per-GPU share at 8 GPUs: 128 x 16 MiB frames (2 GiB), 16
+    sessions; round trip over the whole batch, oracle on three frames."""
+    torch = torch_cuda
+    n, P, ns = 128, 16 << 20, 16
+    W = P + 33
+    keys = _keys(ns, 44)
+    enc, dec = _contexts(C, keys)
+    i = torch.arange(n, device="cuda", dtype=torch.int64)
+    sid = (i % ns).to(torch.int32)
+    nonce = 3 + i // ns
+    flags = (i % 16 == 15).to(torch.uint8)
+    lens = torch.full((n,), P, dtype=torch.int32, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(45)
+    payload = torch.randint(0, 256, (n * P,), dtype=torch.uint8, device="cuda", generator=g)
+    wire = torch.zeros(n * W, dtype=torch.uint8, device="cuda")
+    enc.encode_batch(sid, nonce, flags, i * P, lens, payload, i * W, wire)
+    back = torch.zeros(n * P, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    wl = torch.full((n,), W, dtype=torch.int32, device="cuda")
+    dec.decode_batch(sid, i * W, wl, wire, i * P, back, fl, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert torch.equal(fl, flags) and torch.equal(back, payload)
+    idx = np.array([0, 77, n - 1])
+    _check_sample(torch, keys, idx, idx % ns, 3 + idx // ns, (idx % 16 == 15), P, payload, wire, W)
