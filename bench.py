@@ -18,7 +18,9 @@ JSON line fields beyond the driver contract:
                 GB/s vs the 8 TB/s peak, durations from HIP events recorded
                 live around that kernel on its stream during the timed steps;
                 traffic = PMC-measured HBM bytes per launch from
-                profiles/ if a PMC summary for this workload was committed.
+                profiles/ if a PMC summary for this workload was committed;
+                valu = the same kernel against the VALU issue peak (the bound
+                that binds: PMC instruction count / live launch duration).
   cpu_baseline  the oracle's C restatement of curve_encoding_t with
                 libsodium's crypto_box_easy_afternm/open (dlopen) on host
                 threads, rank 0 at N=1 only, on a bounded sample.
@@ -206,9 +208,28 @@ def main():
                 traffic_write = d.get("write_bytes_per_launch")
         except Exception:
             traffic = traffic_write = None
+    # The kernel is VALU-issue bound: its VALU
+    # instruction count per launch (committed PMC pass) over the same live
+    # launch duration, against the chip's VALU issue peak (1024 SIMDs x 16
+    # lanes per cycle) at the spec clock and at the clock measured under
+    # this load.
+    valu = None
+    pv = os.path.join(ROOT, "profiles", "pmc_valu_config2.json")
+    if os.path.exists(pv) and n == 65536 and P == 1024 and dec_avg_s > 0:
+        try:
+            d = json.load(open(pv))
+            if d.get("kernel") == ROOF_KERNEL:
+                ops = d["valu_wave_instr_per_launch"] * 64 / dec_avg_s
+                peak = d["simds"] * d["lanes_per_simd_per_cycle"] * d["clock_ghz_spec"] * 1e9
+                peak_m = d["simds"] * d["lanes_per_simd_per_cycle"] * d["clock_ghz_measured"] * 1e9
+                valu = {"achieved": ops / 1e12, "peak": peak / 1e12, "unit": "T lane-ops/s", "frac": ops / peak,
+                        "frac_at_measured_clock": ops / peak_m, "clock_ghz_measured": d["clock_ghz_measured"],
+                        "lane_ops_per_frame": d["valu_lane_ops_per_frame"]}
+        except Exception:
+            valu = None
     roofline = {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None, "traffic": traffic,
-                "traffic_write": traffic_write,
+                "traffic_write": traffic_write, "valu": valu,
                 "algorithmic_bytes_per_launch": dec_read, "avg_launch_us": dec_avg_s * 1e6,
                 "encode_main_avg_us": enc_avg_s * 1e6,
                 "encode_call_avg_us": enc_call_ms / max(enc_body_n, 1) * 1e3,
