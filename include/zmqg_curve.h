@@ -226,6 +226,34 @@ int zmqg_scalarmult_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *scalar, cons
 int zmqg_box_beforenm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *pk, const uint8_t *sk, uint8_t *k_out,
                             int32_t *status_out, void *stream);
 
+/* Handshake boxes in batches: every CURVE
+ * command body is one crypto_box / crypto_secretbox with its own key and
+ * 24-byte nonce -- HELLO (src/curve_client_tools.hpp:45), WELCOME
+ * (src/curve_server.cpp:232, opened at src/curve_client_tools.hpp:92), the
+ * cookie (src/curve_server.cpp:208, :334), INITIATE's vouch and box
+ * (src/curve_client_tools.hpp:140, :177; src/curve_server.cpp:291, :359) and
+ * READY (src/curve_server.cpp:441, src/curve_client.cpp:206).  With
+ * crypto_box(pk, sk) = crypto_box_afternm(crypto_box_beforenm(pk, sk)) and
+ * crypto_secretbox(k) = crypto_box_afternm(k) (libsodium 1.0.18), these two
+ * calls plus zmqg_box_beforenm_batch seal and open all of them.  Item i:
+ * key[32i .. +32], nonce[24i .. +24], input in[in_off[i] .. +len[i]], output
+ * at out[out_off[i]] (the "easy" layouts: no NaCl zero padding).
+ *   zmqg_box_afternm_batch: crypto_box_easy_afternm -- writes
+ *     tag(16) || ciphertext(len[i]).
+ *   zmqg_box_open_afternm_batch: crypto_box_open_easy_afternm -- reads
+ *     tag || ciphertext (len[i] bytes), writes len[i] - 16 plaintext bytes,
+ *     status_out[i] = 0; -1 where len[i] < 16 or the tag does not verify
+ *     (checked before any plaintext is written; the region is then
+ *     zero-filled).
+ * One thread per box; inputs and outputs must not overlap.  Asynchronous on
+ * `stream`; pointers as for the batch calls. */
+int zmqg_box_afternm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *key, const uint8_t *nonce,
+                           const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                           uint8_t *out, void *stream);
+int zmqg_box_open_afternm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *key, const uint8_t *nonce,
+                                const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
+                                const uint64_t *out_off, uint8_t *out, int32_t *status_out, void *stream);
+
 /* Batched Z85 key codec: zmq_z85_encode /
  * zmq_z85_decode (src/zmq_utils.cpp:100-180, include/zmq.h:537-540) over n
  * independent items, one per thread.  Item i: input bytes

@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "../../include/zmqg_curve.h"
+#include "curve_box.hpp"
 #include "curve_device.hpp"
 #include "curve_frames.hpp"
 #include "curve_z85.hpp"
@@ -1988,6 +1989,40 @@ int zmqg_box_beforenm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *pk, const 
     ZCHECK(ctx, hipSetDevice(ctx->device));
     hipLaunchKernelGGL(k_beforenm, dim3((unsigned) ((n + 63) / 64)), dim3(64), 0, (hipStream_t) stream,
                        (uint32_t) n, pk, sk, k_out, status_out);
+    ZCHECK(ctx, hipGetLastError());
+    return 0;
+}
+
+int zmqg_box_afternm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *key, const uint8_t *nonce,
+                           const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                           uint8_t *out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!key || !nonce || !in_off || !len || !in || !out_off || !out)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_box<false>, dim3((unsigned) ((n + 63) / 64)), dim3(64), 0, (hipStream_t) stream,
+                       (uint32_t) n, key, nonce, in_off, len, in, out_off, out, (int32_t *) nullptr);
+    ZCHECK(ctx, hipGetLastError());
+    return 0;
+}
+
+int zmqg_box_open_afternm_batch(zmqg_ctx *ctx, uint64_t n, const uint8_t *key, const uint8_t *nonce,
+                                const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
+                                const uint64_t *out_off, uint8_t *out, int32_t *status_out, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!key || !nonce || !in_off || !len || !in || !out_off || !out || !status_out)
+        return -EINVAL;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_box<true>, dim3((unsigned) ((n + 63) / 64)), dim3(64), 0, (hipStream_t) stream,
+                       (uint32_t) n, key, nonce, in_off, len, in, out_off, out, status_out);
     ZCHECK(ctx, hipGetLastError());
     return 0;
 }

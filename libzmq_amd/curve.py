@@ -66,6 +66,8 @@ _lib.zmqg_decode_zmtp.argtypes = [_P, _U32, _P, _U64, ctypes.c_int64, _U64] + [_
                                                                                        _P]
 _lib.zmqg_scalarmult_batch.argtypes = [_P, _U64] + [_P] * 5
 _lib.zmqg_box_beforenm_batch.argtypes = [_P, _U64] + [_P] * 5
+_lib.zmqg_box_afternm_batch.argtypes = [_P, _U64] + [_P] * 8
+_lib.zmqg_box_open_afternm_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_z85_encode_batch.argtypes = [_P, _U64] + [_P] * 7
 _lib.zmqg_z85_decode_batch.argtypes = [_P, _U64] + [_P] * 7
 _lib.zmqg_host_alloc.argtypes = [_P, _U64, ctypes.POINTER(_P)]
@@ -217,6 +219,23 @@ class CurveContext:
         n = int(status_out.numel())
         self._check(_lib.zmqg_box_beforenm_batch(self._ctx, n, _ptr(pk), _ptr(sk), _ptr(k_out), _ptr(status_out),
                                                  _stream_handle(stream)), "zmqg_box_beforenm_batch")
+
+    # ---- handshake boxes: crypto_box_easy_afternm / _open_ per item ----
+    def box_afternm_batch(self, key, nonce, in_off, length, inp, out_off, out, stream=None):
+        """Seal: out[out_off[i]] = tag || ciphertext of in[in_off[i] .. +length[i]]
+        under key[i] (32 B) and nonce[i] (24 B)."""
+        n = int(in_off.numel())
+        self._check(_lib.zmqg_box_afternm_batch(self._ctx, n, _ptr(key), _ptr(nonce), _ptr(in_off), _ptr(length),
+                                                _ptr(inp), _ptr(out_off), _ptr(out), _stream_handle(stream)),
+                    "zmqg_box_afternm_batch")
+
+    def box_open_afternm_batch(self, key, nonce, in_off, length, inp, out_off, out, status_out, stream=None):
+        """Open: length[i] = 16 + plaintext bytes; status 0 or -1."""
+        n = int(in_off.numel())
+        self._check(_lib.zmqg_box_open_afternm_batch(self._ctx, n, _ptr(key), _ptr(nonce), _ptr(in_off),
+                                                     _ptr(length), _ptr(inp), _ptr(out_off), _ptr(out),
+                                                     _ptr(status_out), _stream_handle(stream)),
+                    "zmqg_box_open_afternm_batch")
 
     # ---- batched Z85 (zmq_z85_encode / zmq_z85_decode), device tensors ----
     def z85_encode_batch(self, in_off, length, inp, out_off, out, status_out, stream=None):
