@@ -41,10 +41,16 @@
 #define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: 1 no Poly1305, 2 no stores, 4 no input shift
 #endif
 
+#ifndef ZMQG_FR_BS
+#define ZMQG_FR_BS 256 // frame-kernel workgroup size (threads)
+#endif
+
 #include "../../include/zmqg_curve.h"
 #include "curve_device.hpp"
 
 namespace zmqg {
+
+constexpr uint32_t kFramesBS = ZMQG_FR_BS, kFramesWaves = kFramesBS / 64;
 
 struct DevSession {
     uint32_t enc_key[8]; // HSalsa20(precom, enc_prefix)
@@ -283,7 +289,7 @@ struct ZState {
 };
 
 // Decoupled look-back, whole workgroup: maximum of the aggregates of every
-// workgroup ticket < t, reading 256 tickets per round (one per thread) and
+// workgroup ticket < t, reading kFramesBS tickets per round (one per thread) and
 // stopping at the nearest one that has published its inclusive value.
 // Every earlier ticket has started (tickets are taken at workgroup start)
 // and publishes its aggregate right after its header pass, so the spin is
@@ -294,11 +300,11 @@ __device__ __forceinline__ unsigned long long lookback_excl(uint32_t t, uint32_t
                                                             const unsigned long long *lb_agg,
                                                             const unsigned long long *lb_inc)
 {
-    __shared__ uint32_t sh_stop[4];
-    __shared__ unsigned long long sh_v[4];
+    __shared__ uint32_t sh_stop[kFramesWaves];
+    __shared__ unsigned long long sh_v[kFramesWaves];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     unsigned long long P = 0;
-    for (int base = (int) t; base > 0; base -= 256) {
+    for (int base = (int) t; base > 0; base -= (int) kFramesBS) {
         const int k = base - 1 - (int) tid; // this thread's predecessor
         int state = 2;                      // out of range: an inclusive zero
         if (k >= 0) {
@@ -313,10 +319,10 @@ __device__ __forceinline__ unsigned long long lookback_excl(uint32_t t, uint32_t
             v = __hip_atomic_load((state == 2 ? lb_inc : lb_agg) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long m = __ballot(state == 2);
         if (lane == 0)
-            sh_stop[wv] = m ? 64u * wv + (uint32_t) __builtin_ctzll(m) : 256u;
+            sh_stop[wv] = m ? 64u * wv + (uint32_t) __builtin_ctzll(m) : kFramesBS;
         __syncthreads();
-        uint32_t stop = 256;
-        for (int w = 0; w < 4; ++w)
+        uint32_t stop = kFramesBS;
+        for (uint32_t w = 0; w < kFramesWaves; ++w)
             stop = sh_stop[w] < stop ? sh_stop[w] : stop;
         if (tid > stop)
             v = 0;
@@ -328,10 +334,10 @@ __device__ __forceinline__ unsigned long long lookback_excl(uint32_t t, uint32_t
         if (lane == 0)
             sh_v[wv] = v;
         __syncthreads();
-        for (int w = 0; w < 4; ++w)
+        for (uint32_t w = 0; w < kFramesWaves; ++w)
             P = sh_v[w] > P ? sh_v[w] : P;
         __syncthreads();
-        if (stop < 256)
+        if (stop < kFramesBS)
             break;
     }
     return P;
@@ -361,7 +367,7 @@ struct NoBigFrames {
 // zs: the context's call state (see ZState); decode with rp.lb_flag set
 // applies the one-session replay rule in this kernel.
 template <bool DEC, int G, class BigOp>
-__global__ __launch_bounds__(256) void k_frames(
+__global__ __launch_bounds__(kFramesBS) void k_frames(
     uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
     const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
@@ -377,7 +383,7 @@ __global__ __launch_bounds__(256) void k_frames(
     }
     uint32_t wg = blockIdx.x;
     __shared__ uint32_t sh_ticket, sh_epoch;
-    __shared__ unsigned long long sh_wmax[4];
+    __shared__ unsigned long long sh_wmax[kFramesWaves];
     if (threadIdx.x == 0) {
         // the epoch first: it only advances after every workgroup has finished
         sh_epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(256) void k_frames(
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0; // the next call's list (the previous body has finished with it)
-    const uint32_t gl = wg * 256u + threadIdx.x;
+    const uint32_t gl = wg * kFramesBS + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t i = gl / G, q = gl % G;
     const uint32_t gbase = lane - q; // the group's lane 0
@@ -463,7 +469,7 @@ __global__ __launch_bounds__(256) void k_frames(
                 sh_wmax[threadIdx.x >> 6] = sc;
             __syncthreads();
             const uint32_t wv = threadIdx.x >> 6;
-            for (uint32_t k = 0; k < 4; ++k) {
+            for (uint32_t k = 0; k < kFramesWaves; ++k) {
                 if (k < wv)
                     wexcl = sh_wmax[k] > wexcl ? sh_wmax[k] : wexcl;
                 wagg = sh_wmax[k] > wagg ? sh_wmax[k] : wagg;

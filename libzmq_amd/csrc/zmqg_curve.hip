@@ -1332,9 +1332,9 @@ int frames_capacity(zmqg_ctx *ctx, int G)
     int &c = ctx->frames_cap[G == 1 ? 0 : G == 2 ? 1 : 2];
     if (c == 0) {
         int nb = 0;
-        hipError_t e = G == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, 256, 0)
-                       : G == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, 256, 0)
-                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 4, DecodeHead>, 256, 0);
+        hipError_t e = G == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
+                       : G == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, kFramesBS, 0)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 4, DecodeHead>, kFramesBS, 0);
         c = (e == hipSuccess && nb > 0) ? nb * ctx->cus : -1;
     }
     return c;
@@ -1346,9 +1346,9 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
                    const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
                    uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs)
 {
-    const dim3 grid((uint32_t) (((uint64_t) n * G + 255) / 256));
+    const dim3 grid((uint32_t) (((uint64_t) n * G + kFramesBS - 1) / kFramesBS));
 #define ZMQG_LAUNCH_FRAMES(GG)                                                                                        \
-    hipLaunchKernelGGL((k_frames<DEC, GG, BigOp>), grid, dim3(256), 0, st, n, sid, nonce, flags, in_off, len, in,      \
+    hipLaunchKernelGGL((k_frames<DEC, GG, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,      \
                        out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs)
     if (G == 1)
         ZMQG_LAUNCH_FRAMES(1);
@@ -1636,7 +1636,7 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         // A grid that fits the device at once can use blockIdx as the
         // look-back order (every workgroup becomes resident eventually,
         // whatever the dispatch order); a larger one takes tickets.
-        const uint64_t grid = ((uint64_t) nn * G + 255) / 256;
+        const uint64_t grid = ((uint64_t) nn * G + kFramesBS - 1) / kFramesBS;
         rp.ordered = grid <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
     }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
