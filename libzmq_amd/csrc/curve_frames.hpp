@@ -286,6 +286,8 @@ struct ZState {
     uint32_t done;
     uint32_t pad;
     unsigned long long list_ctr[2]; // big frames << 40 | body chunks, by epoch parity
+    uint32_t body_done;             // decode body kernel: workgroups past their release
+    uint32_t body_fail;             // decode body kernel: failed big frames listed
 };
 
 // Decoupled look-back, whole workgroup: maximum of the aggregates of every

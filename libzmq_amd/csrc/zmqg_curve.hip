@@ -76,6 +76,7 @@ namespace {
 constexpr uint32_t kChunk = 128;      // body chunk: 2 Salsa20 blocks = 8 Poly1305 blocks per lane
 constexpr int kMaxPow = 25;           // r^(8*2^k), k < 25: frames up to 2^32 bytes
 constexpr uint32_t kIdle = 0xffffffffu;
+constexpr uint64_t kBodySegTiles = 32768; // body tiles per segment: 256 MiB of chunks (see k_body)
 constexpr int kBodyThreads = 256; // 4 waves x 2 tile buffers of 9 KiB: 2 workgroups (8 waves) per CU
 constexpr int kHeadThreads = 256;
 constexpr uint32_t kMaxFrameStream = 64 * 72; // frames up to 4.5 KiB of stream: frame kernel
@@ -135,6 +136,7 @@ struct Workspace {
     uint32_t *keys_s = nullptr;   // [cap]
     uint8_t *last = nullptr;      // [cap] last frame of its session in the batch
     uint32_t *list_frame = nullptr;      // [cap] big-frame list: frame index at each position
+    uint32_t *fail = nullptr;            // [cap] decode body: list positions of failed big frames
     unsigned long long *psnap = nullptr; // [cap] session peer nonce before the batch, per frame
     unsigned long long *blockmax = nullptr; // [cap] frame-kernel workgroup maxima of vout
     ZState *zs = nullptr;                   // call state carried from call to call (on the device)
@@ -489,15 +491,25 @@ __device__ __forceinline__ bool frame_combine(uint32_t g0, uint32_t nch, unsigne
     const uint32_t w0 = g0 >> 6, w1 = (g0 + nch - 1) >> 6;
     if (w0 == w1)
         return true; // the whole frame is inside this wave's segment
+    // No fences: the partial sums and the arrival counter are agent-scope
+    // atomics, performed at the one coherence point every XCD's atomics to
+    // an address go through.  Each wave's adds have returned before its
+    // counter add issues, so the wave whose counter add returns last finds
+    // every partial in acc, and reads them back with atomic adds of zero.
+    // (An acq_rel counter add here -- buffer_wbl2 of the XCD's L2 per tile
+    // -- made frames spanning tiles 5x slower.)
+    unsigned long long ret[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q)
-        __hip_atomic_fetch_add(acc + q, (unsigned long long) sum[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        ret[q] = __hip_atomic_fetch_add(acc + q, (unsigned long long) sum[q], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(ret[0]), "v"(ret[1]), "v"(ret[2]), "v"(ret[3]), "v"(ret[4]) : "memory");
+    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old != w1 - w0)
         return false;
 #pragma unroll
     for (int q = 0; q < 5; ++q)
-        sum[q] = __hip_atomic_load(acc + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sum[q] = __hip_atomic_fetch_add(acc + q, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
 }
 
@@ -954,15 +966,51 @@ __device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t
     }
 }
 
+// Decode: zero-fill the payload region of every big frame that failed (the
+// finishers listed them in fail_list).  A failed frame's tiles may have left
+// plaintext dirty in other XCDs' L2s, to be written back at any time, so the
+// zeroing waits for all of them: each workgroup releases its stores once at
+// its end (one L2 write-back per workgroup, not per tile) and counts itself;
+// the last one acquires, clears the listed frames and resets the counters.
+__device__ void zero_failed_frames(ZState *zs, const uint32_t *__restrict__ fail_list,
+                                   const FrameFin *__restrict__ fin, const FrameHot *__restrict__ hot)
+{
+    __shared__ uint32_t sh_nf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t d = __hip_atomic_fetch_add(&zs->body_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_nf = 0xffffffffu;
+        if (d + 1u == gridDim.x) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            sh_nf = __hip_atomic_load(&zs->body_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&zs->body_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&zs->body_fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    const uint32_t nf = sh_nf;
+    if (nf == 0xffffffffu)
+        return;
+    for (uint32_t f = 0; f < nf; ++f) {
+        const uint32_t q = fail_list[f];
+        uint8_t *o = (uint8_t *) (uintptr_t) hot[q].out_base;
+        const uint32_t len = fin[q].wire_len - 33u;
+        for (uint32_t b = threadIdx.x; b < len; b += kBodyThreads)
+            o[b] = 0;
+    }
+}
+
 // The big-frame list (positions 0 .. n-1, built by the frame kernel's head
 // calls) is read from the call state: n = entries, total = body chunks.
 template <bool DEC>
 __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_body(
-    const ZState *__restrict__ zs, const uint32_t *__restrict__ chunk_end,
+    ZState *__restrict__ zs, const uint32_t *__restrict__ chunk_end,
     const FrameHot *__restrict__ hot, const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
     const uint32_t *__restrict__ powtab, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
     unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
-    const unsigned long long *__restrict__ psnap)
+    const unsigned long long *__restrict__ psnap, uint32_t *__restrict__ fail_list)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kBufLds];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -974,9 +1022,17 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         return;
     const uint64_t tiles = (total + 63) >> 6;
     const uint64_t W = (uint64_t) blockIdx.x * kBodyWaves + wv, NW = (uint64_t) gridDim.x * kBodyWaves;
-    const uint32_t tb = (uint32_t) (tiles * W / NW), te = (uint32_t) (tiles * (W + 1) / NW);
+    // The tiles go in segments of kBodySegTiles; each wave takes a contiguous
+    // share of every segment.  One share of the whole list per wave would
+    // spread the running waves over the entire batch: past ~0.5 GiB of big
+    // frames their pages no longer fit the address translation caches and
+    // the kernel ran 5x slower.  A segment keeps them within 256 MiB.
+#pragma unroll 1
+    for (uint64_t s0 = 0; s0 < tiles; s0 += kBodySegTiles) {
+    const uint64_t seg = tiles - s0 < kBodySegTiles ? tiles - s0 : kBodySegTiles;
+    const uint32_t tb = (uint32_t) (s0 + seg * W / NW), te = (uint32_t) (s0 + seg * (W + 1) / NW);
     if (tb >= te)
-        return;
+        continue;
 
     // prologue: locate tile tb from scratch, set it up and start its DMA;
     // locate tile tb+1
@@ -1175,11 +1231,10 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
                                                                : 0;
                     status_out[i] = status;
                     flags_out[i] = status == 0 ? (uint8_t) cur.flags : 0;
-                    if (status != 0) {
-                        uint8_t *o = (uint8_t *) (uintptr_t) cur.out_base;
-                        for (uint32_t b = 0; b < wire_len - 33; ++b)
-                            o[b] = 0;
-                    }
+                    if (status != 0) // its payload region is zero-filled at the kernel's end
+                        fail_list[__hip_atomic_fetch_add(&zs->body_fail, 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)] = p;
+                    (void) wire_len;
                 }
             }
         }
@@ -1195,6 +1250,9 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         cur = nx;
         lkn = lk2;
     }
+    } // segment
+    if (DEC)
+        zero_failed_frames(zs, fail_list, fin, hot);
 }
 
 } // namespace
@@ -1228,7 +1286,7 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
             (rc = grow(ctx, w.chunk_end, cap)) || (rc = grow(ctx, w.v, cap)) || (rc = grow(ctx, w.excl, cap)) ||
             (rc = grow(ctx, w.v_s, cap)) || (rc = grow(ctx, w.excl_s, cap)) || (rc = grow(ctx, w.iota, cap)) ||
             (rc = grow(ctx, w.perm, cap)) || (rc = grow(ctx, w.keys_s, cap)) || (rc = grow(ctx, w.last, cap)) ||
-            (rc = grow(ctx, w.list_frame, cap)) || (rc = grow(ctx, w.psnap, cap)) ||
+            (rc = grow(ctx, w.list_frame, cap)) || (rc = grow(ctx, w.fail, cap)) || (rc = grow(ctx, w.psnap, cap)) ||
             (rc = grow(ctx, w.blockmax, cap)) || (rc = grow(ctx, w.lb_flag, cap)) || (rc = grow(ctx, w.lb_agg, cap)) ||
             (rc = grow(ctx, w.lb_inc, cap)))
             return rc;
@@ -1413,7 +1471,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     (void) hipDeviceSynchronize();
     Workspace &w = ctx->ws;
     void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
-                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.psnap, w.blockmax, w.zs,
+                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.fail, w.psnap, w.blockmax, w.zs,
                     w.lb_flag, w.lb_agg, w.lb_inc, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
@@ -1594,7 +1652,8 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
     hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
                        w.pw, w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, w.acc, w.cnt,
-                       (const unsigned long long *) nullptr, (const unsigned long long *) nullptr);
+                       (const unsigned long long *) nullptr, (const unsigned long long *) nullptr,
+                       (uint32_t *) nullptr);
     ZCHECK(ctx, hipGetLastError());
     body.end();
     call.end();
@@ -1662,7 +1721,7 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     }
     ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
     hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
-                       w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap);
+                       w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap, w.fail);
     ZCHECK(ctx, hipGetLastError());
     body.end();
     if (multi) {

@@ -145,3 +145,51 @@ def test_config5_jumbo_per_gpu_share(torch_cuda, C):
     assert torch.equal(fl, flags) and torch.equal(back, payload)
     idx = np.array([0, 77, n - 1])
     _check_sample(torch, keys, idx, idx % ns, 3 + idx // ns, (idx % 16 == 15), P, payload, wire, W)
+
+
+def test_big_frame_failures_zero_filled(torch_cuda, C):
+    """Frames spanning many body tiles that fail (flipped ciphertext bit, flipped
+    tag bit, replayed nonce) get their status and a zero-filled payload region,
+    while the frames around them decode intact (the decode body kernel's
+    end-of-kernel zero-fill after every workgroup's release)."""
+    torch = torch_cuda
+    sizes = [65536, 70000, 1 << 20, 65536, 200000, 65536, 1 << 20, 12288, 65536, 300000]
+    n = len(sizes)
+    keys = _keys(1, 46)
+    enc, dec = _contexts(C, keys)
+    rng = np.random.default_rng(47)
+    pay = [rng.integers(0, 256, s, dtype=np.uint8) for s in sizes]
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    W = np.array(sizes, np.uint64) + 33
+    out_off = np.concatenate([[0], np.cumsum(W)[:-1]]).astype(np.uint64)
+    nonce = np.arange(3, 3 + n, dtype=np.uint64)
+    nonce[6] = nonce[4]  # frame 6 replays frame 4's nonce
+    t = lambda a, d: torch.from_numpy(np.ascontiguousarray(a).view(d)).to("cuda")
+    sid = torch.zeros(n, dtype=torch.int32, device="cuda")
+    flags = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    payload = t(np.concatenate(pay), np.uint8)
+    wire = torch.zeros(int(W.sum()), dtype=torch.uint8, device="cuda")
+    enc.encode_batch(sid, t(nonce, np.int64), flags, t(in_off, np.int64), t(np.array(sizes, np.uint32), np.int32),
+                     payload, t(out_off, np.int64), wire)
+    torch.cuda.synchronize()
+    w = wire.cpu().numpy()
+    w[int(out_off[1]) + 33 + 50000] ^= 4          # ciphertext bit, frame 1 (70 KB)
+    w[int(out_off[2]) + 20] ^= 1                  # tag bit, frame 2 (1 MiB)
+    w[int(out_off[9]) + int(W[9]) - 1] ^= 0x80    # last ciphertext byte, frame 9
+    back = torch.full((int(sum(sizes)),), 0x5A, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    dec.decode_batch(sid, t(out_off, np.int64), t(W.astype(np.uint32), np.int32), t(w, np.uint8),
+                     t(in_off, np.int64), back, fl, st)
+    torch.cuda.synchronize()
+    got = back.cpu().numpy()
+    status = st.cpu().numpy()
+    expect = {1: C.ERR_CRYPTOGRAPHIC, 2: C.ERR_CRYPTOGRAPHIC, 6: C.ERR_INVALID_SEQUENCE, 9: C.ERR_CRYPTOGRAPHIC}
+    for i in range(n):
+        region = got[int(in_off[i]):int(in_off[i]) + sizes[i]]
+        assert status[i] == expect.get(i, 0), (i, status[i])
+        if i in expect:
+            assert not region.any(), i
+        else:
+            assert np.array_equal(region, pay[i]), i
+    assert dec.get_peer_nonce(0) == int(nonce.max())
