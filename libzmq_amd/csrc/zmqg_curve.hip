@@ -76,7 +76,6 @@ namespace {
 constexpr uint32_t kChunk = 128;      // body chunk: 2 Salsa20 blocks = 8 Poly1305 blocks per lane
 constexpr int kMaxPow = 25;           // r^(8*2^k), k < 25: frames up to 2^32 bytes
 constexpr uint32_t kIdle = 0xffffffffu;
-constexpr uint64_t kBodySegTiles = 32768; // body tiles per segment: 256 MiB of chunks (see k_body)
 constexpr int kBodyThreads = 256; // 4 waves x 2 tile buffers of 9 KiB: 2 workgroups (8 waves) per CU
 constexpr int kHeadThreads = 256;
 constexpr uint32_t kMaxFrameStream = 64 * 72; // frames up to 4.5 KiB of stream: frame kernel
@@ -1022,17 +1021,8 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         return;
     const uint64_t tiles = (total + 63) >> 6;
     const uint64_t W = (uint64_t) blockIdx.x * kBodyWaves + wv, NW = (uint64_t) gridDim.x * kBodyWaves;
-    // The tiles go in segments of kBodySegTiles; each wave takes a contiguous
-    // share of every segment.  One share of the whole list per wave would
-    // spread the running waves over the entire batch: past ~0.5 GiB of big
-    // frames their pages no longer fit the address translation caches and
-    // the kernel ran 5x slower.  A segment keeps them within 256 MiB.
-#pragma unroll 1
-    for (uint64_t s0 = 0; s0 < tiles; s0 += kBodySegTiles) {
-    const uint64_t seg = tiles - s0 < kBodySegTiles ? tiles - s0 : kBodySegTiles;
-    const uint32_t tb = (uint32_t) (s0 + seg * W / NW), te = (uint32_t) (s0 + seg * (W + 1) / NW);
-    if (tb >= te)
-        continue;
+    const uint32_t tb = (uint32_t) (tiles * W / NW), te = (uint32_t) (tiles * (W + 1) / NW);
+    if (tb < te) {
 
     // prologue: locate tile tb from scratch, set it up and start its DMA;
     // locate tile tb+1
@@ -1250,7 +1240,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         cur = nx;
         lkn = lk2;
     }
-    } // segment
+    } // tb < te (waves without tiles still take part in the decode zero-fill)
     if (DEC)
         zero_failed_frames(zs, fail_list, fin, hot);
 }
