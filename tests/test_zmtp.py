@@ -151,7 +151,19 @@ def test_decode_zmtp_matches_oracle(torch_cuda, C, case):
     assert (d_foff[:nf].cpu().numpy().view(np.uint64) == f_off).all()
     assert (d_flen[:nf].cpu().numpy().view(np.uint32) == f_len).all()
     assert (d_poff[:nf].cpu().numpy().view(np.uint64) == p_off).all()
-    assert (d_st[:nf].cpu().numpy() == st).all()
+    got_st = d_st[:nf].cpu().numpy()
+    if not (got_st == st).all():  # diagnostics for a rare first-run mismatch seen on fresh boxes
+        bad = np.nonzero(got_st != st)[0]
+        d_st2 = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        ctx2 = C.CurveContext(0, 1)
+        ctx2.session_set(0, precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+        ctx2.decode_zmtp(0, d_in, len(stream), max_msg, max_frames, d_foff, d_flen, d_poff, d_out, d_fl, d_st2)
+        again = d_st2[:nf].cpu().numpy()
+        print("status mismatch at", bad[:16].tolist(), "lens", f_len[bad[:16]].tolist(), "got",
+              [hex(int(x)) for x in got_st[bad[:4]]], "expected", st[bad[:4]].tolist(),
+              "descriptors ok", bool((d_foff[:nf].cpu().numpy().view(np.uint64) == f_off).all()),
+              "re-run mismatches", int((again != st).sum()))
+    assert (got_st == st).all()
     assert (d_fl[:nf].cpu().numpy() == fl).all()
     assert d_out[:int(plen.sum())].cpu().numpy().tobytes() == pl[:int(plen.sum())].tobytes()
     if case in ("clean", "large_small", "zmtp_flags"):
