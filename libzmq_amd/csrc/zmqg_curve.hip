@@ -1288,6 +1288,10 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
             z0.epoch = 1;
             ZCHECK(ctx, hipMemcpy(w.zs, &z0, sizeof z0, hipMemcpyHostToDevice));
         }
+        // hipMemset / hipMemcpy run on the null stream and may still be in
+        // flight when they return; the batch's kernels run on the caller's
+        // stream (possibly non-blocking), so wait for them here (growth only)
+        ZCHECK(ctx, hipDeviceSynchronize());
         w.cap = cap;
     }
     // hipCUB temporaries for n frames
@@ -1440,6 +1444,12 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
         e = hipMalloc((void **) &ctx->peer, sizeof(unsigned long long) * max_sessions);
     if (e == hipSuccess)
         e = hipMemset(ctx->peer, 0, sizeof(unsigned long long) * max_sessions);
+    // the memsets are queued on the null stream, which the ctx's non-blocking
+    // stream does not wait for: without this, a session installed right after
+    // could be zeroed by the late memset (seen as every MAC failing on the
+    // first context of a fresh process)
+    if (e == hipSuccess)
+        e = hipDeviceSynchronize();
     if (e == hipSuccess)
         e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess)
