@@ -290,6 +290,123 @@ __device__ __forceinline__ void poly_absorb64(fe &h, const fe &r, const uint32_t
     }
 }
 
+// ---------------------------------------------------------------- Poly1305, radix 2^32
+// The sequential form h = (h + m) * r with h in four 32-bit words plus a
+// small fifth (h4 <= 6 between blocks) and r clamped: the clamp (r_k < 2^28,
+// r_1..r_3 multiples of 4) keeps every sum of four word products below 2^64
+// and lets 2^130 = 5/4 fold into s_k = r_k + r_k/4.  19 v_mad_u64_u32 and one
+// v_mul_lo_u32 per 16-byte block, against 25 v_mad_u64_u32 plus the limb
+// split of the radix-2^26 form (measured 0.72x the Poly1305 time of that
+// form in the frame loop, tools/frames_proto.hip).
+struct Poly32 {
+    uint32_t h0, h1, h2, h3, h4;
+};
+
+struct PolyKey32 {
+    uint32_t r0, r1, r2, r3, s1, s2, s3;
+};
+
+__device__ __forceinline__ PolyKey32 poly32_key(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3)
+{
+    PolyKey32 k;
+    k.r0 = k0 & 0x0fffffffu;
+    k.r1 = k1 & 0x0ffffffcu;
+    k.r2 = k2 & 0x0ffffffcu;
+    k.r3 = k3 & 0x0ffffffcu;
+    k.s1 = k.r1 + (k.r1 >> 2);
+    k.s2 = k.r2 + (k.r2 >> 2);
+    k.s3 = k.r3 + (k.r3 >> 2);
+    return k;
+}
+
+// h = (h + m + hib * 2^128) * r, partially reduced (h4 <= 4 on return).
+// Carries are 32-bit add-with-carry chains (v_add_co / v_addc_co); written
+// as 64-bit sums the compiler materialises zero high halves and 64-bit adds
+// (245 instructions per window against 165 this way).
+__device__ __forceinline__ void poly32_block(Poly32 &h, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                             uint32_t hib, const PolyKey32 &k)
+{
+    unsigned c;
+    const uint32_t a0 = __builtin_addc(h.h0, m0, 0u, &c);
+    const uint32_t a1 = __builtin_addc(h.h1, m1, c, &c);
+    const uint32_t a2 = __builtin_addc(h.h2, m2, c, &c);
+    const uint32_t a3 = __builtin_addc(h.h3, m3, c, &c);
+    const uint32_t a4 = h.h4 + hib + c;
+    const uint64_t d0 = mad64(a3, k.s1, mad64(a2, k.s2, mad64(a1, k.s3, (uint64_t) a0 * k.r0)));
+    const uint64_t d1 = mad64(a4, k.s1, mad64(a3, k.s2, mad64(a2, k.s3, mad64(a1, k.r0, (uint64_t) a0 * k.r1))));
+    const uint64_t d2 = mad64(a4, k.s2, mad64(a3, k.s3, mad64(a2, k.r0, mad64(a1, k.r1, (uint64_t) a0 * k.r2))));
+    const uint64_t d3 = mad64(a4, k.s3, mad64(a3, k.r0, mad64(a2, k.r1, mad64(a1, k.r2, (uint64_t) a0 * k.r3))));
+    // h = d0 + d1 2^32 + d2 2^64 + d3 2^96 + (a4 r0) 2^128
+    const uint32_t h0 = (uint32_t) d0;
+    const uint32_t h1 = __builtin_addc((uint32_t) d1, (uint32_t) (d0 >> 32), 0u, &c);
+    const uint32_t c1 = (uint32_t) (d1 >> 32) + c;
+    const uint32_t h2 = __builtin_addc((uint32_t) d2, c1, 0u, &c);
+    const uint32_t c2 = (uint32_t) (d2 >> 32) + c;
+    const uint32_t h3 = __builtin_addc((uint32_t) d3, c2, 0u, &c);
+    const uint32_t h4 = a4 * k.r0 + (uint32_t) (d3 >> 32) + c;
+    const uint32_t f = (h4 >> 2) + (h4 & ~3u); // 5 * (h >> 130)
+    h.h0 = __builtin_addc(h0, f, 0u, &c);
+    h.h1 = __builtin_addc(h1, 0u, c, &c);
+    h.h2 = __builtin_addc(h2, 0u, c, &c);
+    h.h3 = __builtin_addc(h3, 0u, c, &c);
+    h.h4 = (h4 & 3u) + c;
+}
+
+// Absorb the ciphertext blocks of one 64-byte keystream window: the window's
+// 16 words c (zero beyond the ciphertext), its first block slot j0 (2 for
+// window 0, whose first 32 stream bytes are the Poly1305 key, else 0) and the
+// ciphertext bytes it holds (len, 1..64).  A final partial block gets the
+// 0x01 pad byte and no 2^128 bit.
+__device__ __forceinline__ void poly32_window(Poly32 &h, const PolyKey32 &k, const uint32_t c[16], uint32_t j0,
+                                              uint32_t len)
+{
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int off = 16 * (j - (int) j0);
+        if (j >= (int) j0 && off < (int) len) {
+            const int nb = (int) len - off;
+            uint32_t m0 = c[4 * j], m1 = c[4 * j + 1], m2 = c[4 * j + 2], m3 = c[4 * j + 3], hib = 1u;
+            if (nb < 16) {
+                hib = 0u;
+                const uint32_t pad = 1u << (8 * (nb & 3));
+                const int wi = nb >> 2;
+                m0 |= wi == 0 ? pad : 0u;
+                m1 |= wi == 1 ? pad : 0u;
+                m2 |= wi == 2 ? pad : 0u;
+                m3 |= wi == 3 ? pad : 0u;
+            }
+            poly32_block(h, m0, m1, m2, m3, hib, k);
+        }
+    }
+}
+
+// The four full blocks of an interior window.
+__device__ __forceinline__ void poly32_window_full(Poly32 &h, const PolyKey32 &k, const uint32_t c[16])
+{
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        poly32_block(h, c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3], 1u, k);
+}
+
+// Tag = (h mod 2^130-5) + s mod 2^128 (h4 <= 4, so one conditional
+// subtraction of p reduces it).
+__device__ __forceinline__ void poly32_finish(const Poly32 &h, const uint32_t s[4], uint32_t tag[4])
+{
+    unsigned c;
+    const uint32_t g0 = __builtin_addc(h.h0, 5u, 0u, &c);
+    const uint32_t g1 = __builtin_addc(h.h1, 0u, c, &c);
+    const uint32_t g2 = __builtin_addc(h.h2, 0u, c, &c);
+    const uint32_t g3 = __builtin_addc(h.h3, 0u, c, &c);
+    const uint32_t g4 = h.h4 + c;
+    const uint32_t m = 0u - (g4 >> 2); // all ones when h + 5 >= 2^130: take h - p
+    const uint32_t f0 = (g0 & m) | (h.h0 & ~m), f1 = (g1 & m) | (h.h1 & ~m), f2 = (g2 & m) | (h.h2 & ~m),
+                   f3 = (g3 & m) | (h.h3 & ~m);
+    tag[0] = __builtin_addc(f0, s[0], 0u, &c);
+    tag[1] = __builtin_addc(f1, s[1], c, &c);
+    tag[2] = __builtin_addc(f2, s[2], c, &c);
+    tag[3] = __builtin_addc(f3, s[3], c, &c);
+}
+
 // ---------------------------------------------------------------- bytes
 // Little-endian word of 4 bytes from a byte pointer (any alignment).
 __device__ __forceinline__ uint32_t bswap32(uint32_t x)
@@ -384,6 +501,24 @@ __device__ __forceinline__ void store_window(uint8_t *p, int nv, const uint32_t 
     }
 }
 
+
+// Zero bytes [p, p + len) by one lane: byte stores up to the first 16-byte
+// boundary and after the last, dwordx4 stores between.  (Only for regions a
+// lane may afford to clear alone: a frame the frame kernel holds, at most a
+// few KiB; larger regions go to the cooperative fill kernel.)
+__device__ __forceinline__ void zero_bytes(uint8_t *p, uint32_t len)
+{
+    const uint32_t head = (uint32_t) ((16u - ((uintptr_t) p & 15u)) & 15u);
+    const uint32_t h = head < len ? head : len;
+    for (uint32_t b = 0; b < h; ++b)
+        p[b] = 0;
+    uint32_t k = h;
+    typedef unsigned int z4 __attribute__((ext_vector_type(4)));
+    for (; k + 16u <= len; k += 16u)
+        *(z4 *) (p + k) = (z4){0u, 0u, 0u, 0u};
+    for (; k < len; ++k)
+        p[k] = 0;
+}
 
 // ---------------------------------------------------------------- streams
 // Global-address-space views (keep global_load/store, not flat, for

@@ -51,6 +51,20 @@
 namespace zmqg {
 
 constexpr uint32_t kFramesBS = ZMQG_FR_BS, kFramesWaves = kFramesBS / 64;
+#ifndef ZMQG_SEQ_STAMPS
+#define ZMQG_SEQ_STAMPS 0 // diagnostic builds only (tools/seq_stamps.hip): per-wave s_memtime stamps into rp.clk, 64 per wave
+#endif
+
+#if ZMQG_SEQ_STAMPS
+#define SEQ_STAMP(slot)                                                                            \
+    do {                                                                                           \
+        if (rp.clk && (threadIdx.x & 63u) == 0 && (slot) < 64u)                                    \
+            rp.clk[64ull * (blockIdx.x * kFramesWaves + (threadIdx.x >> 6)) + (slot)] =            \
+                __builtin_amdgcn_s_memtime();                                                      \
+    } while (0)
+#else
+#define SEQ_STAMP(slot) do { } while (0)
+#endif
 
 struct DevSession {
     uint32_t enc_key[8]; // HSalsa20(precom, enc_prefix)
@@ -800,10 +814,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     if (S == 0) { // decode: header failure
         status_out[i] = status;
         flags_out[i] = 0;
-        if (L_in >= 33u) { // zero-filled payload region
-            for (uint32_t b = 0; b < L_in - 33u; ++b)
-                dst[b] = 0;
-        }
+        if (L_in >= 33u) // zero-filled payload region
+            zero_bytes(dst, L_in - 33u);
         return;
     }
     uint64_t wide[5];
@@ -824,8 +836,452 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
         flags_out[i] = status == 0 ? (uint8_t) fl : 0;
         if (status != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the group's plaintext stores first
-            for (uint32_t b = 0; b < S - 33u; ++b)
-                dst[b] = 0;
+            zero_bytes(dst, S - 33u);
+        }
+    }
+}
+
+// Prefetch of words 1..16 of window w of a stream read in order (word 0 is
+// the previous window's word 16): dd[k] = the aligned word at A4 + 64w +
+// 4(k+1) (kept apart from word 0 so that they are an even register tuple),
+// four dwordx4, issued only where all 16 words are readable -- inside the
+// frame, or below the end of the wave's furthest frame (the caller's buffer
+// covers every frame, so reading up to that end stays inside it).  Returns
+// false where it issued nothing: that lane reloads its words exactly
+// (frame_load_exact) in the step that uses them.  The prefetch writes dd only
+// through these loads, so dd keeps the loads' register tuples from step to
+// step (a second writer of dd, e.g. a select, makes the compiler copy the
+// tuples and wait for the loads right where they are issued).
+__device__ __forceinline__ bool frame_prefetch(uint64_t A4, uint32_t lim, uint64_t wave_end, uint32_t w,
+                                               uint32_t dd[16])
+{
+    const uint64_t a = A4 + 64ull * w;
+    const bool ok = 64u * w + 68u <= lim || a + 68ull <= wave_end;
+    if (ok) {
+        const GCU4a4 *p = (const GCU4a4 *) (uintptr_t) (a + 4ull);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32x4 tt = p[k];
+            dd[4 * k] = tt.x;
+            dd[4 * k + 1] = tt.y;
+            dd[4 * k + 2] = tt.z;
+            dd[4 * k + 3] = tt.w;
+        }
+    }
+    return ok;
+}
+
+// Words 1..16 of window w read one by one, a word past the stream's last one
+// from the last word's address instead (its bytes are >= S: masked or never
+// stored), so no word outside the stream is touched.
+__device__ __forceinline__ void frame_load_exact(uint64_t A4, uint32_t lim, uint32_t w, uint32_t dd[16])
+{
+    const uint32_t last = (lim - 1u) & ~3u; // offset of the last word holding a stream byte
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t o = 64u * w + 4u * (k + 1);
+        dd[k] = *(GCU32 *) (uintptr_t) (A4 + (o <= last ? o : last));
+    }
+}
+
+// ---------------------------------------------------------------- one lane per frame
+// Sequential frame kernel: one lane owns one frame and walks its keystream
+// windows in order (64 frames per wave), with Poly1305 in the sequential
+// radix-2^32 form (curve_device.hpp poly32_*): no powers of r, no
+// cross-lane traffic, and a window's last output word carried in a
+// register to the next window's store.  Measured against the G-lanes kernel
+// (k_frames) and its cost model in tools/frames_proto.hip, DESIGN.md
+// section 3:
+//   * The MAC of window w is absorbed in step w+1, unconditionally in the
+//     keystream's basic block, so the scheduler interleaves its multiply and
+//     carry chains with the Salsa20 rounds (at the batch sizes this kernel
+//     is chosen for, a wave is alone on its SIMD).
+//   * Each step issues the next window's loads and this window's stores
+//     together after the input has been consumed: the wait for them comes a
+//     whole Salsa20 block later (vmcnt counts loads and stores together, so
+//     an earlier wait would drain the stores too).  Issuing them before the
+//     keystream instead (stores one step late) measured no faster in this
+//     kernel, with the loads branch-free or not.
+//   * Decode reads window 0 (header, nonce, tag, first ciphertext) in one
+//     load with the header checks taken from it; encode fetches the payload's
+//     first bytes with the descriptors.
+// Same frame semantics, replay rule, big-frame hand-off and call state as
+// k_frames with G = 1.
+template <bool DEC, class BigOp>
+__global__ __launch_bounds__(kFramesBS) void k_frames_seq(
+    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
+    const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
+    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
+    uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
+    ReplayOut rp, BigOp big, ZState *__restrict__ zs)
+{
+    const bool lb = DEC && rp.lb_flag != nullptr;
+    SEQ_STAMP(0u);
+    uint32_t wg = blockIdx.x;
+    __shared__ uint32_t sh_ticket, sh_epoch;
+    __shared__ unsigned long long sh_wmax[kFramesWaves];
+    if (threadIdx.x == 0) {
+        sh_epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lb && !rp.ordered)
+            sh_ticket = atomicAdd(&zs->ticket, 1u);
+    }
+    __syncthreads();
+    const uint32_t epoch = sh_epoch;
+    if (lb && !rp.ordered)
+        wg = sh_ticket;
+    unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t i = wg * kFramesBS + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t ii = valid ? i : n - 1;
+    const uint32_t s = sid[ii] < max_sessions ? sid[ii] : 0u;
+    const DevSession &ses = sessions[s];
+    uint32_t key[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        key[t] = DEC ? ses.dec_key[t] : ses.enc_key[t];
+    const uint8_t *src = in + in_off[ii];
+    uint8_t *dst = out + out_off[ii];
+    const uint32_t L_in = len[ii];
+
+    uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
+    uint64_t A = 0, B = 0;
+    int32_t status = 0;
+    uint32_t hw[3] = {0, 0, 0};
+    uint32_t x0[16], d0 = 0; // window 0's stream words (decode: the wire; encode: payload bytes 0..), word 16
+    if (!DEC) {
+        const uint64_t nc = nonce[ii];
+        n0 = bswap32((uint32_t) (nc >> 32));
+        n1 = bswap32((uint32_t) nc);
+        hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
+        S = 32u + hl + L_in;
+        A = (uint64_t) (uintptr_t) src - 32u - hl;
+        B = (uint64_t) (uintptr_t) dst;
+        load_window(src, L_in < 32u ? (int) L_in : 32, x0); // payload bytes 0..31
+        if (S > 64u)                                     // word 16: stream bytes 64-v.. (payload)
+            d0 = *(GCU32 *) (uintptr_t) ((A & ~3ull) + 64ull);
+    } else {
+        // the wire frame's first window: header, nonce, tag, 32 ciphertext bytes
+        A = (uint64_t) (uintptr_t) src;
+        uint32_t d[17];
+        frame_load_raw(A, 0, L_in, d);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            x0[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], (uint32_t) A & 3u);
+        d0 = d[16];
+        if (L_in < 64u)
+            mask_tail(x0, (int) L_in);
+        // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
+        const uint32_t b0 = x0[0] & 0xffu;
+        if (L_in <= 1u || L_in <= b0)
+            status = ZMQG_ERR_MALFORMED_UNSPECIFIED;
+        else if (L_in < 8u || x0[0] != 0x53454d07u || x0[1] != 0x45474153u)
+            status = ZMQG_ERR_UNEXPECTED_COMMAND;
+        else if (L_in < 33u)
+            status = ZMQG_ERR_MALFORMED_MESSAGE;
+        n0 = x0[2];
+        n1 = x0[3];
+        S = status == 0 ? L_in : 0u;
+        B = (uint64_t) (uintptr_t) dst - 33u;
+    }
+    const bool small = valid && S <= max_stream;
+    unsigned long long vn = 0, wexcl = 0, psn = 0, wagg = 0;
+    if (DEC) {
+        vn = valid && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
+        psn = rp.peer[s];
+        if (valid) {
+            rp.vout[i] = vn;
+            rp.psnap[i] = psn;
+            if (rp.iota)
+                rp.iota[i] = i;
+        }
+        if (lb) {
+            unsigned long long sc = vn;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const unsigned long long o = __shfl_up(sc, d);
+                if ((int) lane >= d)
+                    sc = o > sc ? o : sc;
+            }
+            const unsigned long long up = __shfl_up(sc, 1);
+            if (lane == 63)
+                sh_wmax[threadIdx.x >> 6] = sc;
+            __syncthreads();
+            const uint32_t wv = threadIdx.x >> 6;
+            for (uint32_t k = 0; k < kFramesWaves; ++k) {
+                if (k < wv)
+                    wexcl = sh_wmax[k] > wexcl ? sh_wmax[k] : wexcl;
+                wagg = sh_wmax[k] > wagg ? sh_wmax[k] : wagg;
+            }
+            if (lane > 0)
+                wexcl = up > wexcl ? up : wexcl;
+            if (threadIdx.x == 0)
+                lookback_publish(rp.lb_flag + wg, rp.lb_agg + wg, wagg, epoch, 1);
+        }
+    }
+    const bool is_big = valid && !small && S > 0;
+    if (!small)
+        S = 0;
+    const uint32_t nw = (S + 63u) >> 6;
+    uint32_t mx = nw;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(mx, d);
+        mx = o > mx ? o : mx;
+    }
+    const uint32_t steps = __builtin_amdgcn_readfirstlane(mx);
+    const uint32_t v = (uint32_t) A & 3u;
+    const uint64_t A4 = A & ~3ull;
+    const uint32_t lim = S + v; // stream words whose first byte is below lim hold a stream byte
+    uint64_t wave_end = nw ? A + S : 0; // end of the wave's furthest frame: reads below it stay in the buffer
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        const uint64_t o = __shfl_xor(wave_end, sh);
+        wave_end = o > wave_end ? o : wave_end;
+    }
+    // window 1's words (word 0 is window 0's word 16, d0); windows t and t+1
+    // alternate between the two buffers
+    uint32_t ddA[16], ddB[16];
+    bool fastA = nw > 1u ? frame_prefetch(A4, lim, wave_end, 1u, ddA) : true, fastB = true;
+
+    SEQ_STAMP(1u);
+    // ---- step 0: window 0 (Poly1305 key, first 32 ciphertext bytes, header)
+    PolyKey32 pk;
+    Poly32 h = {0, 0, 0, 0, 0};
+    uint32_t spad[4], wtag[4] = {0, 0, 0, 0}, fl = 0;
+    uint32_t cp[16];  // ciphertext of the window whose MAC is absorbed next step
+    uint32_t cp_j0 = 2, cp_len = 0; // its first block slot and ciphertext bytes
+    uint32_t ycarry;  // last output word of the previous window
+    {
+        uint32_t ks[16];
+        salsa20_block(ks, key, n0, n1, 0, 0);
+        pk = poly32_key(ks[0], ks[1], ks[2], ks[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            spad[k] = ks[4 + k];
+        uint32_t x[16];
+        if (DEC) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                x[k] = x0[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                wtag[k] = x[4 + k];
+        } else {
+            // plaintext bytes 0..31 = header || payload[0 .. 32-hl)
+            uint32_t pt[8];
+            switch (hl) {
+            case 1: shift_in<1>(x0, pt); break;
+            case 2: shift_in<2>(x0, pt); break;
+            case 8: shift_in<8>(x0, pt); break;
+            default: shift_in<11>(x0, pt); break;
+            }
+            pt[0] |= hw[0];
+            pt[1] |= hw[1];
+            pt[2] |= hw[2];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x[k] = 0;
+                x[8 + k] = pt[k];
+            }
+        }
+        uint32_t y[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            y[k] = x[k] ^ ks[k];
+        if (!DEC && S < 64u)
+            mask_tail(y, (int) S);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            cp[k] = DEC ? x[k] : y[k];
+        cp_len = (S < 64u ? S : 64u) - 32u; // (S = 0: unused)
+        ycarry = y[15];
+        if (nw > 0) {
+            if (DEC) {
+                fl = y[8] & 3u;
+                // payload bytes 0 .. min(31, S-33) = plaintext bytes 1..
+                uint32_t pay[16];
+#pragma unroll
+                for (int k = 0; k < 7; ++k)
+                    pay[k] = __builtin_amdgcn_alignbyte(y[9 + k], y[8 + k], 1);
+                pay[7] = __builtin_amdgcn_alignbyte(0u, y[15], 1);
+#pragma unroll
+                for (int k = 8; k < 16; ++k)
+                    pay[k] = 0;
+                store_window(dst, (int) (S < 64u ? S : 64u) - 33, pay);
+            } else {
+                uint32_t o[16];
+                o[0] = 0x53454d07u; // "\x07MESSAGE" || nonce
+                o[1] = 0x45474153u;
+                o[2] = n0;
+                o[3] = n1;
+#pragma unroll
+                for (int k = 4; k < 16; ++k)
+                    o[k] = 0;
+                store_window(dst, 16, o);
+                uint32_t ct[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    ct[k] = k < 8 ? y[8 + k] : 0u;
+                store_window(dst + 32, (int) (S < 64u ? S : 64u) - 32, ct);
+            }
+        }
+    }
+    SEQ_STAMP(2u);
+
+    // ---- steps 1 ..: window t (words in dd, prefetched by the previous
+    // step; the two buffers alternate so that the loads keep their register
+    // tuples)
+    auto step = [&](uint32_t t, uint32_t (&dd)[16], bool &fast, uint32_t (&dn)[16], bool &fastn) {
+        SEQ_STAMP(3u + t);
+        const bool act = t < nw;
+        uint32_t ks[16];
+        salsa20_block(ks, key, n0, n1, t, 0);
+        // The previous window's MAC (its ciphertext is in cp).  The
+        // four-block form runs for every lane, unconditionally, so that it
+        // shares a basic block with the keystream and the scheduler
+        // interleaves the two; lanes whose window was not four full blocks
+        // keep h and take the general form below.
+        const bool pv = t - 1u < nw;
+        const bool full = pv && cp_j0 == 0u && cp_len == 64u;
+        {
+            Poly32 hf = h;
+            poly32_window_full(hf, pk, cp);
+            h.h0 = full ? hf.h0 : h.h0;
+            h.h1 = full ? hf.h1 : h.h1;
+            h.h2 = full ? hf.h2 : h.h2;
+            h.h3 = full ? hf.h3 : h.h3;
+            h.h4 = full ? hf.h4 : h.h4;
+        }
+        // (keystream and MAC are pinned here, ahead of the next branch:
+        // left to itself the compiler sinks them into later blocks -- the
+        // keystream below the wait for this window's words)
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            asm volatile("" : "+v"(ks[k]));
+        asm volatile("" : "+v"(h.h0), "+v"(h.h1), "+v"(h.h2), "+v"(h.h3), "+v"(h.h4));
+        if (__builtin_amdgcn_ballot_w64(pv && !full) != 0) {
+            if (pv && !full)
+                poly32_window(h, pk, cp, cp_j0, cp_len);
+        }
+        SEQ_STAMP(24u + t);
+        uint32_t x[16], w16; // w16: this window's word 16 = the next window's word 0
+        if (__builtin_amdgcn_ballot_w64(act && !fast) != 0) {
+            // a lane whose words were not prefetched (the end of the wave's
+            // furthest frame) reads them exactly
+            uint32_t ee[16];
+            if (act && !fast)
+                frame_load_exact(A4, lim, t, ee);
+            const bool ex = act && !fast;
+            uint32_t e0 = ex ? ee[0] : dd[0];
+            x[0] = __builtin_amdgcn_alignbyte(e0, d0, v);
+#pragma unroll
+            for (int k = 1; k < 16; ++k) {
+                const uint32_t ek = ex ? ee[k] : dd[k];
+                x[k] = __builtin_amdgcn_alignbyte(ek, e0, v);
+                e0 = ek;
+            }
+            w16 = e0;
+        } else {
+            x[0] = __builtin_amdgcn_alignbyte(dd[0], d0, v);
+#pragma unroll
+            for (int k = 1; k < 16; ++k)
+                x[k] = __builtin_amdgcn_alignbyte(dd[k], dd[k - 1], v);
+            w16 = dd[15];
+        }
+        d0 = w16;
+        const bool tail = act && S < 64u * t + 64u;
+        if (DEC && __builtin_amdgcn_ballot_w64(tail) != 0) {
+            if (tail)
+                mask_tail(x, (int) (S - 64u * t));
+        }
+        uint32_t y[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            y[k] = x[k] ^ ks[k];
+        if (!DEC && __builtin_amdgcn_ballot_w64(tail) != 0) {
+            if (tail)
+                mask_tail(y, (int) (S - 64u * t));
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            cp[k] = DEC ? x[k] : y[k];
+        cp_j0 = 0;
+        cp_len = act ? (S - 64u * t < 64u ? S - 64u * t : 64u) : 0u;
+        // window t+1's loads and window t's stores, issued together after
+        // the input has been consumed: the wait for the loads comes a whole
+        // keystream later
+        if (t + 1u < nw)
+            fastn = frame_prefetch(A4, lim, wave_end, t + 1u, dn);
+        if (act)
+            frame_store(B, t, S, y, ycarry, t + 1u == nw);
+        ycarry = y[15];
+    };
+#pragma unroll 1
+    for (uint32_t t = 1; t < steps; t += 2) {
+        step(t, ddA, fastA, ddB, fastB);
+        if (t + 1u < steps)
+            step(t + 1u, ddB, fastB, ddA, fastA);
+    }
+    SEQ_STAMP(60u);
+    // the last window's MAC
+    if (steps > 0 && nw == steps)
+        poly32_window(h, pk, cp, cp_j0, cp_len);
+
+    unsigned long long excl = 0;
+    if (lb) {
+        const unsigned long long P = lookback_excl(wg, epoch, rp.lb_flag, rp.lb_agg, rp.lb_inc);
+        if (threadIdx.x == 0) {
+            const unsigned long long inc = P > wagg ? P : wagg;
+            lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
+            if (wg + 1 == gridDim.x)
+                *rp.peer = inc > psn ? inc : psn;
+        }
+        excl = P > wexcl ? P : wexcl;
+        if (excl < psn)
+            excl = psn;
+    }
+    if (is_big) {
+        if (lb)
+            rp.excl[i] = excl;
+        big(i, list_ctr);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(&zs->done, 1u) + 1u == gridDim.x) {
+            __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    SEQ_STAMP(61u);
+    if (!valid || !small)
+        return;
+    if (S == 0) { // decode: header failure
+        status_out[i] = status;
+        flags_out[i] = 0;
+        if (L_in >= 33u)
+            zero_bytes(dst, L_in - 33u);
+        return;
+    }
+    uint32_t tag[4];
+    poly32_finish(h, spad, tag);
+    if (!DEC) {
+        uint32_t o[16] = {tag[0], tag[1], tag[2], tag[3]};
+        store_window(dst + 16, 16, o);
+    } else {
+        if (lb && !(vn > excl))
+            status = ZMQG_ERR_INVALID_SEQUENCE; // src/curve_mechanism_base.cpp:99-104 (before the MAC)
+        else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
+            status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
+        status_out[i] = status;
+        flags_out[i] = status == 0 ? (uint8_t) fl : 0;
+        if (status != 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this lane's plaintext stores first
+            zero_bytes(dst, S - 33u);
         }
     }
 }

@@ -190,7 +190,8 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
-    int frames_cap[3] = {0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4
+    int frames_cap[4] = {0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4, seq
+    int force_g = -1;                 // ZMQG_FRAMES_G: frame-kernel variant override (experiments)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
     // completion fences of the asynchronous host path: (id, event) pending,
@@ -1370,21 +1371,27 @@ struct ProfSpan {
     }
 };
 
-// Lanes per frame for the frame kernel: enough waves for >= 2 per SIMD.
-int lanes_per_frame(uint32_t n)
+// Frame-kernel variant: 0 = one lane per frame (k_frames_seq: batches that
+// give every SIMD at least one wave), else G lanes per frame (k_frames) so
+// that a smaller batch still spreads over the chip.  ZMQG_FRAMES_G (0, 1, 2,
+// 4) forces a variant (experiments, tests).
+int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 {
-    return n >= 131072u ? 1 : n >= 32768u ? 2 : 4;
+    if (ctx->force_g >= 0)
+        return ctx->force_g;
+    return n >= 65536u ? 0 : n >= 32768u ? 2 : 4;
 }
 
 // Workgroups of the decode frame kernel the device holds at once (occupancy
 // query x CUs; the kernel is VGPR-limited, where the query is exact --
-// MI355X_MICROARCH.md, Residency), cached per G.
+// MI355X_MICROARCH.md, Residency), cached per variant.
 int frames_capacity(zmqg_ctx *ctx, int G)
 {
-    int &c = ctx->frames_cap[G == 1 ? 0 : G == 2 ? 1 : 2];
+    int &c = ctx->frames_cap[G == 0 ? 3 : G == 1 ? 0 : G == 2 ? 1 : 2];
     if (c == 0) {
         int nb = 0;
-        hipError_t e = G == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
+        hipError_t e = G == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
+                       : G == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
                        : G == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, kFramesBS, 0)
                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 4, DecodeHead>, kFramesBS, 0);
         c = (e == hipSuccess && nb > 0) ? nb * ctx->cus : -1;
@@ -1398,7 +1405,12 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
                    const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
                    uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs)
 {
-    const dim3 grid((uint32_t) (((uint64_t) n * G + kFramesBS - 1) / kFramesBS));
+    const dim3 grid((uint32_t) (((uint64_t) n * (G ? G : 1) + kFramesBS - 1) / kFramesBS));
+    if (G == 0) {
+        hipLaunchKernelGGL((k_frames_seq<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
+                           out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs);
+        return;
+    }
 #define ZMQG_LAUNCH_FRAMES(GG)                                                                                        \
     hipLaunchKernelGGL((k_frames<DEC, GG, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,      \
                        out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs)
@@ -1435,6 +1447,11 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
         ++bits;
     ctx->sort_bits = bits;
     ctx->h_downgrade.assign(max_sessions, 0);
+    if (const char *fg = getenv("ZMQG_FRAMES_G")) {
+        const int g = atoi(fg);
+        if (g == 0 || g == 1 || g == 2 || g == 4)
+            ctx->force_g = g;
+    }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess)
         e = hipMalloc((void **) &ctx->sessions, sizeof(DevSession) * max_sessions);
@@ -1638,7 +1655,7 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         return rc;
     Workspace &w = ctx->ws;
     const uint32_t nn = (uint32_t) n;
-    const int G = lanes_per_frame(nn);
+    const int G = lanes_per_frame(ctx, nn);
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_ENCODE_MAIN, st);
@@ -1678,7 +1695,7 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     Workspace &w = ctx->ws;
     const uint32_t nn = (uint32_t) n;
     const dim3 hgrid((nn + kHeadThreads - 1) / kHeadThreads);
-    const int G = lanes_per_frame(nn);
+    const int G = lanes_per_frame(ctx, nn);
     const bool multi = ctx->sort_bits > 0;
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ReplayOut rp{};
@@ -1695,7 +1712,7 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         // A grid that fits the device at once can use blockIdx as the
         // look-back order (every workgroup becomes resident eventually,
         // whatever the dispatch order); a larger one takes tickets.
-        const uint64_t grid = ((uint64_t) nn * G + kFramesBS - 1) / kFramesBS;
+        const uint64_t grid = ((uint64_t) nn * (G ? G : 1) + kFramesBS - 1) / kFramesBS;
         rp.ordered = grid <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
     }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);

@@ -1,0 +1,107 @@
+// Phase timing of the one-lane-per-frame kernel (k_frames_seq), diagnostic
+// build (-DZMQG_SEQ_STAMPS=1): per wave, s_memtime at entry (0), before
+// window 0 (1), after it (2), at the start of step t (3+t) and after the
+// wait for step t's input words (24+t), after the loop (60), at the end
+// (61); for steps 1..7 also before the prefetch (44+t) and before the
+// stores (52+t).  Config-2 shape: 65,536 frames of 1 KiB, encode then decode.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DZMQG_SEQ_STAMPS=1 -o build/seq_stamps tools/seq_stamps.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <vector>
+#include <algorithm>
+#include "../libzmq_amd/csrc/curve_frames.hpp"
+using namespace zmqg;
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+int main()
+{
+    const uint32_t n = 65536, P = 1024, W = P + 33;
+    std::vector<uint32_t> sid(n, 0), len(n, P), wl(n, W);
+    std::vector<uint64_t> nonce(n), ioff(n), ooff(n);
+    std::vector<uint8_t> flags(n, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        nonce[i] = 3 + i;
+        ioff[i] = (uint64_t) i * P;
+        ooff[i] = (uint64_t) i * W;
+    }
+    auto dev = [](const void *h, size_t b) {
+        void *d = nullptr;
+        if (hipMalloc(&d, b + 256) != hipSuccess || hipMemcpy(d, h, b, hipMemcpyHostToDevice) != hipSuccess)
+            return (void *) nullptr;
+        return d;
+    };
+    uint32_t *d_sid = (uint32_t *) dev(sid.data(), 4 * n), *d_len = (uint32_t *) dev(len.data(), 4 * n),
+             *d_wl = (uint32_t *) dev(wl.data(), 4 * n);
+    uint64_t *d_nonce = (uint64_t *) dev(nonce.data(), 8 * n), *d_ioff = (uint64_t *) dev(ioff.data(), 8 * n),
+             *d_ooff = (uint64_t *) dev(ooff.data(), 8 * n);
+    uint8_t *d_flags = (uint8_t *) dev(flags.data(), n);
+    uint8_t *d_pay, *d_wire, *d_back, *d_fl;
+    int32_t *d_st;
+    CHECK(hipMalloc(&d_pay, (size_t) n * P + 256));
+    CHECK(hipMemset(d_pay, 0x3c, (size_t) n * P + 256));
+    CHECK(hipMalloc(&d_wire, (size_t) n * W + 256));
+    CHECK(hipMalloc(&d_back, (size_t) n * P + 256));
+    CHECK(hipMalloc(&d_fl, n));
+    CHECK(hipMalloc(&d_st, 4 * n));
+    DevSession *d_ses;
+    CHECK(hipMalloc(&d_ses, sizeof(DevSession)));
+    CHECK(hipMemset(d_ses, 0x11, sizeof(DevSession)));
+    ZState *d_zs;
+    CHECK(hipMalloc(&d_zs, sizeof(ZState)));
+    ZState z0{};
+    z0.epoch = 1;
+    CHECK(hipMemcpy(d_zs, &z0, sizeof z0, hipMemcpyHostToDevice));
+    unsigned long long *d_v, *d_clk;
+    CHECK(hipMalloc(&d_v, 32ull * n + 64));
+    CHECK(hipMemset(d_v, 0, 32ull * n + 64));
+    const size_t nwaves = n / 64;
+    CHECK(hipMalloc(&d_clk, 8 * 64 * nwaves));
+    ReplayOut rp{};
+    rp.vout = d_v;
+    rp.psnap = d_v + n;
+    rp.peer = d_v + 3 * n;
+    const dim3 grid(n / kFramesBS);
+    for (int dec = 0; dec < 2; ++dec) {
+        for (int rep = 0; rep < 3; ++rep) {
+            CHECK(hipMemset(d_clk, 0, 8 * 64 * nwaves));
+            rp.clk = rep == 2 ? d_clk : nullptr;
+            if (!dec)
+                hipLaunchKernelGGL((k_frames_seq<false, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid, d_nonce,
+                                   d_flags, d_ioff, d_len, d_pay, d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr,
+                                   nullptr, rp, NoBigFrames{}, d_zs);
+            else
+                hipLaunchKernelGGL((k_frames_seq<true, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid,
+                                   (const uint64_t *) nullptr, (const uint8_t *) nullptr, d_ooff, d_wl, d_wire, d_ioff,
+                                   d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, NoBigFrames{}, d_zs);
+            CHECK(hipDeviceSynchronize());
+        }
+        std::vector<unsigned long long> c(64 * nwaves);
+        CHECK(hipMemcpy(c.data(), d_clk, 8 * 64 * nwaves, hipMemcpyDeviceToHost));
+        // per slot: median over waves of (stamp - entry stamp), and of step deltas
+        printf("%s: median cycles since entry per phase (min/median/max over waves)\n", dec ? "decode" : "encode");
+        std::vector<int> slots = {1, 2};
+        for (int t = 1; t <= 16; ++t) {
+            slots.push_back(3 + t);
+            slots.push_back(24 + t);
+            if (t < 8) {
+                slots.push_back(44 + t);
+                slots.push_back(52 + t);
+            }
+        }
+        slots.push_back(60);
+        slots.push_back(61);
+        for (int sl : slots) {
+            std::vector<long long> v;
+            for (size_t w = 0; w < nwaves; ++w)
+                if (c[64 * w + sl])
+                    v.push_back((long long) (c[64 * w + sl] - c[64 * w]));
+            if (v.empty())
+                continue;
+            std::sort(v.begin(), v.end());
+            printf("  slot %2d: %8lld %8lld %8lld\n", sl, v.front(), v[v.size() / 2], v.back());
+        }
+    }
+    return 0;
+}
