@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define ZMQG_CURVE_ABI_VERSION 1
+#define ZMQG_CURVE_ABI_VERSION 2
 
 /* Per-frame status codes, identical to include/zmq.h:424-437. */
 #define ZMQG_STATUS_OK 0
@@ -64,6 +64,15 @@ extern "C" {
 #define ZMQG_ERR_MALFORMED_UNSPECIFIED 0x10000011 /* ..._MALFORMED_COMMAND_UNSPECIFIED */
 #define ZMQG_ERR_MALFORMED_MESSAGE 0x10000012   /* ..._MALFORMED_COMMAND_MESSAGE */
 #define ZMQG_ERR_CRYPTOGRAPHIC 0x11000001       /* ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC */
+/* Library codes (not protocol errors; the reference has no equivalent):
+ * ZMQG_ERR_SESSION  sid[i] >= the ctx's max_sessions (the frame is not
+ *                   processed; decode: payload region zero-filled as for a
+ *                   header failure)
+ * ZMQG_ERR_BOUND    the frame is longer than zmqg_batch_opts.max_len (the
+ *                   caller's promise was broken; the frame is not processed
+ *                   and its output region is left as it was) */
+#define ZMQG_ERR_SESSION 0x7a000001
+#define ZMQG_ERR_BOUND 0x7a000002
 
 /* msg_t flag bits used on this path (src/msg.hpp:55-62). */
 #define ZMQG_MSG_MORE 1
@@ -92,8 +101,9 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx);
 int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], const uint8_t enc_prefix[16],
                      const uint8_t dec_prefix[16], int downgrade_sub, uint64_t peer_nonce);
 
-/* curve_encoding_t::set_peer_nonce / read back _cn_peer_nonce.  Synchronous
- * (they order after all work previously issued on the ctx's last stream). */
+/* curve_encoding_t::set_peer_nonce / read back _cn_peer_nonce.  Synchronous:
+ * they are ordered after the work previously issued on the stream of the
+ * ctx's last batch call (no device-wide synchronisation). */
 int zmqg_session_set_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t peer_nonce);
 int zmqg_session_get_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *peer_nonce_out);
 
@@ -107,7 +117,9 @@ uint64_t zmqg_wire_size(uint8_t msg_flags, int downgrade_sub, uint64_t payload_l
  * nonce nonce[i], msg_t flags flags[i], payload in[in_off[i] .. +len[i]).
  * Writes zmqg_wire_size(flags[i], session.downgrade_sub, len[i]) bytes at
  * out[out_off[i]]: "\x07MESSAGE" || BE64(nonce) || tag || ciphertext.
- * Output frames must not overlap each other or the input. */
+ * Output frames must not overlap each other or the input.  sid[i] must be
+ * below max_sessions: a frame with another sid is not encoded (its output
+ * region is left as it was; zmqg_encode_batch_ex reports it). */
 int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
                       const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
                       uint8_t *out, void *stream);
@@ -121,10 +133,68 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  * wire_len[i] >= 33, the payload region is zero-filled: plaintext of a frame
  * that failed is never left in `out`.  Each session's peer nonce advances as
  * the reference's check_validity does (src/curve_mechanism_base.cpp:98-106,
- * including on a later MAC failure).  `out` must not overlap `in`. */
+ * including on a later MAC failure).
+ *
+ * In-place decode: `out` may be `in`, with every frame in one of the two
+ * layouts the reference produces (src/curve_mechanism_base.cpp:222-260):
+ * out_off[i] = in_off[i] + 33, the payload where crypto_box_open_easy_afternm
+ * leaves it, or out_off[i] = in_off[i], the payload at the frame's start as
+ * after the reference's memmove.  Otherwise `out` must not overlap `in`.  On
+ * failure the payload region is zero-filled as above; in the second layout a
+ * frame of more than 4.5 KiB that fails has its whole wire region zeroed.
+ *
+ * Unauthenticated plaintext: the kernels decrypt and authenticate in one
+ * pass, so until the call has completed on its stream, `out` may hold
+ * plaintext of frames that then fail (it is zeroed before completion).  The
+ * reference's libsodium verifies first and writes nothing for a forged frame
+ * (SURVEY.md a12).  Results at completion are identical; a caller whose
+ * `out` is visible to another party while the call runs (e.g. mapped host
+ * memory read by a second thread) must not read it before completion. */
 int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
                       const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
                       uint8_t *flags_out, int32_t *status_out, void *stream);
+
+/* Options of the _ex batch calls (every field optional: a zeroed struct, or
+ * opts = NULL, gives the plain calls' behaviour).
+ *   size             sizeof(zmqg_batch_opts) (ABI check)
+ *   max_len          0, or a bound on every len[i] (encode) / wire_len[i]
+ *                    (decode).  A bound under which every frame fits the frame
+ *                    kernel (stream <= 4.5 KiB: decode wire_len <= 4608, encode
+ *                    len <= 4565) lets the call skip the large-frame kernels
+ *                    (two fewer launches).  A frame above the bound fails with
+ *                    ZMQG_ERR_BOUND.
+ *   status_out       encode only: n entries (device-accessible), 0 or
+ *                    ZMQG_ERR_SESSION / ZMQG_ERR_BOUND per frame.
+ *   session_max_out  decode only: max_sessions entries (device-accessible):
+ *                    per session, the largest header-valid nonce among this
+ *                    batch's frames (0 where it has none) -- the value a rank
+ *                    contributes to shard.peer_prefix when a session's frames
+ *                    span GPUs. */
+typedef struct zmqg_batch_opts {
+    uint32_t size;
+    uint32_t reserved;
+    uint64_t max_len;
+    int32_t *status_out;
+    uint64_t *session_max_out;
+} zmqg_batch_opts;
+int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                         const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                         uint8_t *out, const zmqg_batch_opts *opts, void *stream);
+int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                         const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
+                         uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts, void *stream);
+
+/* Header pass of a sharded decode: writes
+ * session_max_out[s] (max_sessions entries, device-accessible) = the largest
+ * header-valid nonce among the n wire frames of session s (0 where none).
+ * When one session's frames are split over ranks (GPUs), rank r decodes its
+ * slice after setting each session's peer nonce to max(peer before the batch,
+ * the session maxima of ranks < r) -- the exclusive max-scan over ranks of
+ * these vectors (libzmq_amd/shard.py peer_prefix) -- and the slices' results
+ * equal one decode of the whole batch.  Reads 16 bytes per frame.
+ * Asynchronous on `stream`. */
+int zmqg_session_max_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                           const uint32_t *wire_len, const uint8_t *in, uint64_t *session_max_out, void *stream);
 
 /* Host-memory convenience forms of the two batch calls: every pointer is
  * ordinary (pageable) host memory.  They stage through the ctx's pinned

@@ -287,6 +287,7 @@ struct ReplayOut {
                               //    their look-back order (no ticket)
     uint32_t dbg;             // timing experiments only (tools/frames_bench): 1 no look-back, 2 no ticket
     unsigned long long *clk;  // diagnostics only: per workgroup {start, end} s_memrealtime, memtime delta, hw ids
+    unsigned long long *smax; // one session, optional: the batch's largest header-valid nonce (last workgroup)
 };
 
 // Per-context device state that carries from one batch call to the next,
@@ -300,9 +301,45 @@ struct ZState {
     uint32_t done;
     uint32_t pad;
     unsigned long long list_ctr[2]; // big frames << 40 | body chunks, by epoch parity
-    uint32_t body_done;             // decode body kernel: workgroups past their release
-    uint32_t body_fail;             // decode body kernel: failed big frames listed
+    uint32_t post_n;                // decode: entries in the post list (k_post resets it)
+    uint32_t post_done;             // k_post: workgroups finished
 };
+
+// Decode work after the body kernel (k_post, zmqg_curve.hip): zero-fill a
+// failed frame's region, or move an in-place frame's payload from where the
+// body wrote it (wire offset 33) to the frame's start (dst = src - 33).
+constexpr uint32_t kPostZero = 0, kPostMove = 1;
+struct PostOp {
+    uint64_t dst;
+    uint64_t len;
+    uint32_t kind;
+    uint32_t p; // move: the frame's big-list position (its scratch for the segment seams)
+};
+
+__device__ __forceinline__ void post_append(ZState *zs, PostOp *post, uint64_t dst, uint64_t len, uint32_t kind,
+                                            uint32_t p)
+{
+    const uint32_t e = __hip_atomic_fetch_add(&zs->post_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PostOp o;
+    o.dst = dst;
+    o.len = len;
+    o.kind = kind;
+    o.p = p;
+    post[e] = o;
+}
+
+// Per-call options of the frame kernels (zmqg_batch_opts, include/zmqg_curve.h).
+struct FrameCtl {
+    int32_t *enc_status; // encode: per-frame 0 / ZMQG_ERR_SESSION / ZMQG_ERR_BOUND (optional)
+    PostOp *post;        // decode: header-failed frames too long for one lane to zero-fill
+    uint64_t max_len;    // 0, or the caller's bound on len / wire_len
+    uint32_t no_body;    // 1: no body kernel follows (every frame within max_len fits this kernel)
+    uint32_t pad;
+};
+
+// Frames whose region a failing lane zero-fills itself; longer ones go to
+// the post list (k_post spreads them over the whole grid).
+constexpr uint32_t kLaneFillMax = 4608;
 
 // Decoupled look-back, whole workgroup: maximum of the aggregates of every
 // workgroup ticket < t, reading kFramesBS tickets per round (one per thread) and
@@ -371,6 +408,24 @@ __device__ __forceinline__ void lookback_publish(unsigned long long *flag, unsig
     __hip_atomic_store(flag, ((unsigned long long) epoch << 2) | state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Decode result of a frame whose stream was not processed (header failure,
+// unknown session, broken bound): status, flags 0, and the payload region
+// zero-filled -- by this lane up to kLaneFillMax bytes, above that by k_post
+// over the whole grid (a forged 16 MiB header must not cost one lane 16 MiB
+// of stores).  A frame above the caller's bound is left as it was.
+__device__ __forceinline__ void fail_unprocessed(int32_t status, uint32_t L_in, uint8_t *dst, uint8_t *flags_out,
+                                                 int32_t *status_out, ZState *zs, const FrameCtl &ctl)
+{
+    *status_out = status;
+    *flags_out = 0;
+    if (status == ZMQG_ERR_BOUND || L_in < 33u)
+        return;
+    if (L_in - 33u <= kLaneFillMax || ctl.post == nullptr)
+        zero_bytes(dst, L_in - 33u);
+    else
+        post_append(zs, ctl.post, (uint64_t) (uintptr_t) dst, L_in - 33u, kPostZero, 0);
+}
+
 // No big-frame handler (tools, tests): frames above max_stream are skipped.
 struct NoBigFrames {
     __device__ void operator()(uint32_t, unsigned long long *) const {}
@@ -388,7 +443,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
     uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
-    ReplayOut rp, BigOp big, ZState *__restrict__ zs)
+    ReplayOut rp, BigOp big, ZState *__restrict__ zs, FrameCtl ctl)
 {
     static_assert(G == 1 || G == 2 || G == 4, "lanes per frame");
     const bool lb = DEC && rp.lb_flag != nullptr;
@@ -419,7 +474,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     const uint32_t gbase = lane - q; // the group's lane 0
     const bool valid = i < n;
     const uint32_t ii = valid ? i : n - 1;
-    const uint32_t s = sid[ii] < max_sessions ? sid[ii] : 0u;
+    const bool sid_ok = sid[ii] < max_sessions;
+    const uint32_t s = sid_ok ? sid[ii] : 0u; // (a frame of an unknown session is not processed)
     const DevSession &ses = sessions[s];
     uint32_t key[8];
 #pragma unroll
@@ -428,6 +484,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     const uint8_t *src = in + in_off[ii];
     uint8_t *dst = out + out_off[ii];
     const uint32_t L_in = len[ii];
+    const bool over = ctl.max_len != 0 && L_in > ctl.max_len; // the caller's bound broken
 
     uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
     uint64_t A = 0, B = 0;
@@ -438,7 +495,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
         n0 = bswap32((uint32_t) (nc >> 32));
         n1 = bswap32((uint32_t) nc);
         hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
-        S = 32u + hl + L_in;
+        S = sid_ok && !over ? 32u + hl + L_in : 0u;
         A = (uint64_t) (uintptr_t) src - 32u - hl;
         B = (uint64_t) (uintptr_t) dst;
     } else {
@@ -452,6 +509,10 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
             status = ZMQG_ERR_UNEXPECTED_COMMAND;
         else if (L_in < 33u)
             status = ZMQG_ERR_MALFORMED_MESSAGE;
+        if (!sid_ok)
+            status = ZMQG_ERR_SESSION;
+        if (over)
+            status = ZMQG_ERR_BOUND;
         n0 = h16[2];
         n1 = h16[3];
         S = status == 0 ? L_in : 0u;
@@ -778,14 +839,17 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
         if (threadIdx.x == 0) {
             const unsigned long long inc = P > wagg ? P : wagg;
             lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
-            if (wg + 1 == gridDim.x) // _cn_peer_nonce after the batch
+            if (wg + 1 == gridDim.x) { // _cn_peer_nonce after the batch
                 *rp.peer = inc > psn ? inc : psn;
+                if (rp.smax)
+                    *rp.smax = inc;
+            }
         }
         excl = P > wexcl ? P : wexcl;
         if (excl < psn)
             excl = psn;
     }
-    if (is_big && q == 0) {
+    if (is_big && q == 0 && !ctl.no_body) {
         if (lb)
             rp.excl[i] = excl;
         big(i, list_ctr);
@@ -809,13 +873,13 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
             __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    if (!DEC && valid && q == 0 && ctl.enc_status)
+        ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
     if (!valid || q != 0 || !small)
         return;
-    if (S == 0) { // decode: header failure
-        status_out[i] = status;
-        flags_out[i] = 0;
-        if (L_in >= 33u) // zero-filled payload region
-            zero_bytes(dst, L_in - 33u);
+    if (S == 0) { // decode: header failure (encode: a frame not processed)
+        if (DEC)
+            fail_unprocessed(status, L_in, dst, flags_out + i, status_out + i, zs, ctl);
         return;
     }
     uint64_t wide[5];
@@ -913,7 +977,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
     uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
-    ReplayOut rp, BigOp big, ZState *__restrict__ zs)
+    ReplayOut rp, BigOp big, ZState *__restrict__ zs, FrameCtl ctl)
 {
     const bool lb = DEC && rp.lb_flag != nullptr;
     SEQ_STAMP(0u);
@@ -936,7 +1000,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     const uint32_t i = wg * kFramesBS + threadIdx.x;
     const bool valid = i < n;
     const uint32_t ii = valid ? i : n - 1;
-    const uint32_t s = sid[ii] < max_sessions ? sid[ii] : 0u;
+    const bool sid_ok = sid[ii] < max_sessions;
+    const uint32_t s = sid_ok ? sid[ii] : 0u; // (a frame of an unknown session is not processed)
     const DevSession &ses = sessions[s];
     uint32_t key[8];
 #pragma unroll
@@ -945,6 +1010,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     const uint8_t *src = in + in_off[ii];
     uint8_t *dst = out + out_off[ii];
     const uint32_t L_in = len[ii];
+    const bool over = ctl.max_len != 0 && L_in > ctl.max_len; // the caller's bound broken
 
     uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
     uint64_t A = 0, B = 0;
@@ -956,7 +1022,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         n0 = bswap32((uint32_t) (nc >> 32));
         n1 = bswap32((uint32_t) nc);
         hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
-        S = 32u + hl + L_in;
+        S = sid_ok && !over ? 32u + hl + L_in : 0u;
         A = (uint64_t) (uintptr_t) src - 32u - hl;
         B = (uint64_t) (uintptr_t) dst;
         load_window(src, L_in < 32u ? (int) L_in : 32, x0); // payload bytes 0..31
@@ -981,6 +1047,10 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             status = ZMQG_ERR_UNEXPECTED_COMMAND;
         else if (L_in < 33u)
             status = ZMQG_ERR_MALFORMED_MESSAGE;
+        if (!sid_ok)
+            status = ZMQG_ERR_SESSION;
+        if (over)
+            status = ZMQG_ERR_BOUND;
         n0 = x0[2];
         n1 = x0[3];
         S = status == 0 ? L_in : 0u;
@@ -1236,14 +1306,17 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         if (threadIdx.x == 0) {
             const unsigned long long inc = P > wagg ? P : wagg;
             lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
-            if (wg + 1 == gridDim.x)
+            if (wg + 1 == gridDim.x) {
                 *rp.peer = inc > psn ? inc : psn;
+                if (rp.smax)
+                    *rp.smax = inc;
+            }
         }
         excl = P > wexcl ? P : wexcl;
         if (excl < psn)
             excl = psn;
     }
-    if (is_big) {
+    if (is_big && !ctl.no_body) {
         if (lb)
             rp.excl[i] = excl;
         big(i, list_ctr);
@@ -1258,13 +1331,13 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         }
     }
     SEQ_STAMP(61u);
+    if (!DEC && valid && ctl.enc_status)
+        ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
     if (!valid || !small)
         return;
-    if (S == 0) { // decode: header failure
-        status_out[i] = status;
-        flags_out[i] = 0;
-        if (L_in >= 33u)
-            zero_bytes(dst, L_in - 33u);
+    if (S == 0) { // decode: header failure (encode: a frame not processed)
+        if (DEC)
+            fail_unprocessed(status, L_in, dst, flags_out + i, status_out + i, zs, ctl);
         return;
     }
     uint32_t tag[4];

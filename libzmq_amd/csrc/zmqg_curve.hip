@@ -92,11 +92,12 @@ struct __attribute__((aligned(16))) FrameHot { // needed to start a chunk (96 B)
     uint32_t hl;      // encode: plaintext header length (1, 2, 8 or 11)
     uint32_t n0, n1;  // Salsa20 nonce words (the 8 wire nonce bytes, little-endian)
     int32_t status;   // decode: header status (0 = header ok)
-    uint32_t flags;   // decode: plaintext flags & 3
+    uint32_t flags;   // decode: plaintext flags & 3, | kHotMove
     uint64_t in_base;  // encode: payload byte 0; decode: wire byte 0
     uint64_t out_base; // encode: wire byte 0; decode: payload byte 0
 };
 static_assert(sizeof(FrameHot) == 96, "FrameHot layout");
+constexpr uint32_t kHotMove = 0x80; // decode in place: payload moved from wire offset 33 to 0 by k_post
 
 constexpr int kPowInline = 4; // r^(8*2^k) for k < 4 kept in the record (frames up to 17 chunks)
 struct __attribute__((aligned(16))) FramePow { // chunk factor inputs (112 B)
@@ -135,7 +136,7 @@ struct Workspace {
     uint32_t *keys_s = nullptr;   // [cap]
     uint8_t *last = nullptr;      // [cap] last frame of its session in the batch
     uint32_t *list_frame = nullptr;      // [cap] big-frame list: frame index at each position
-    uint32_t *fail = nullptr;            // [cap] decode body: list positions of failed big frames
+    PostOp *post = nullptr;              // [cap] decode: k_post's zero fills and in-place moves
     unsigned long long *psnap = nullptr; // [cap] session peer nonce before the batch, per frame
     unsigned long long *blockmax = nullptr; // [cap] frame-kernel workgroup maxima of vout
     ZState *zs = nullptr;                   // call state carried from call to call (on the device)
@@ -144,6 +145,9 @@ struct Workspace {
     unsigned long long *lb_inc = nullptr;   // [cap]
     void *temp = nullptr;
     size_t temp_bytes = 0;
+    unsigned long long *rt = nullptr; // replay tables: [tiles][S] then [row blocks][S]
+    size_t rt_cap = 0;
+    bool use_last = false; // the last replay ran the sort fallback (k_fixup writes the peer nonces)
 };
 
 } // namespace
@@ -187,6 +191,7 @@ struct zmqg_ctx {
     uint8_t *dbuf = nullptr;
     size_t dbuf_bytes = 0;
     hipStream_t own_stream = nullptr;
+    hipStream_t last_stream = nullptr; // the stream of the last batch call (peer-nonce accessors order after it)
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
@@ -541,9 +546,17 @@ __device__ void DecodeHead::operator()(uint32_t i, unsigned long long *list_ctr)
     unsigned long long *acc = R.acc;
     uint32_t *cnt = R.cnt;
     const uint32_t wl = wire_len[i];
-    const uint32_t s = sid[i] < max_sessions ? sid[i] : 0;
+    const uint32_t s = sid[i]; // (the frame kernel hands over known sessions only)
     const uint8_t *src = in + in_off[i];
     uint8_t *dst = out + out_off[i];
+    // In-place decode with the payload at the frame's start (the reference's
+    // memmove layout): the body's chunks run in parallel, and a chunk's output
+    // 33 bytes below its input would overwrite ciphertext a neighbouring chunk
+    // may not have read yet.  The body decodes to the wire position instead
+    // (output byte = its own input byte) and k_post moves the payload down.
+    const bool move = dst == src;
+    if (move)
+        dst += 33;
     uint32_t w[16];
     load_window(src, 64, w); // wl > kMaxFrameStream >= 64
     const uint32_t mlen = wl - 32;
@@ -602,7 +615,7 @@ __device__ void DecodeHead::operator()(uint32_t i, unsigned long long *list_ctr)
     H.mlen = mlen;
     H.n0 = w[2];
     H.n1 = w[3];
-    H.flags = pt[0] & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND);
+    H.flags = (pt[0] & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND)) | (move ? kHotMove : 0u);
     store_fe(F.hh, h);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -637,18 +650,20 @@ __global__ void k_scatter_replay(uint32_t n, const uint32_t *__restrict__ perm, 
 // several sessions, as if the frames were decoded one by one in batch
 // order: a header-valid frame passes iff its nonce exceeds max(its session's
 // peer nonce before the batch, every earlier header-valid nonce of that
-// session in the batch) -- excl, from the sort-by-session path; the peer
-// nonce is set before the MAC check, so a MAC failure still advances it.
-// Small frames get INVALID_SEQUENCE, flags 0 and a zero-filled payload here
-// (big frames in the body finisher, which runs before); the last frame of
-// each session writes the session's new peer nonce = max(before, all its
-// header-valid nonces).  (One session: the frame kernel does all of this.)
+// session in the batch) -- excl[i], computed by the replay tables below
+// (k_replay_*); the peer nonce is set before the MAC check, so a MAC failure
+// still advances it.  Small frames get INVALID_SEQUENCE, flags 0 and a
+// zero-filled payload here (big frames in the body finisher, which runs
+// before).  With `last` (the sort fallback), the last frame of each session
+// also writes the session's new peer nonce; the tables write it themselves.
+// (One session: the frame kernel does all of this.)
 __global__ __launch_bounds__(kFixupThreads) void k_fixup(
     uint32_t n, uint32_t max_stream, const unsigned long long *__restrict__ vout,
     const unsigned long long *__restrict__ psnap, const unsigned long long *__restrict__ excl,
     const uint8_t *__restrict__ last, const uint32_t *__restrict__ sid, uint32_t max_sessions,
     const uint32_t *__restrict__ wire_len, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
-    int32_t *__restrict__ status_out, uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ peer)
+    int32_t *__restrict__ status_out, uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ peer,
+    unsigned long long *__restrict__ smax)
 {
     const uint32_t i = blockIdx.x * kFixupThreads + threadIdx.x;
     if (i >= n)
@@ -661,17 +676,172 @@ __global__ __launch_bounds__(kFixupThreads) void k_fixup(
     if (header_ok && wl <= max_stream && !(v > prev) && st != ZMQG_ERR_INVALID_SEQUENCE) {
         status_out[i] = ZMQG_ERR_INVALID_SEQUENCE;
         flags_out[i] = 0;
-        if (st == 0) { // (a MAC failure is already zero-filled)
-            uint8_t *o = out + out_off[i];
-            for (uint32_t b = 0; b + 33 < wl; ++b)
-                o[b] = 0;
-        }
+        if (st == 0) // (a MAC failure is already zero-filled)
+            zero_bytes(out + out_off[i], wl - 33u);
     }
-    if (last[i]) {
-        unsigned long long pn = prev;
+    if (last && last[i] && sid[i] < max_sessions) {
+        unsigned long long pn = prev, bm = ex;
         if (header_ok && v > pn)
             pn = v;
-        peer[sid[i] < max_sessions ? sid[i] : 0] = pn;
+        if (header_ok && v > bm)
+            bm = v;
+        peer[sid[i]] = pn;
+        if (smax)
+            smax[sid[i]] = bm;
+    }
+}
+
+// Header pass for sharded decode: per session, the
+// largest header-valid nonce among n wire frames -- what a rank contributes to
+// the exclusive max-scan over ranks (libzmq_amd/shard.py peer_prefix) before
+// any rank decodes.  Header rule as the frame kernel's
+// (src/mechanism_base.cpp:14-25, src/curve_mechanism_base.cpp:80-97).
+__global__ __launch_bounds__(256) void k_session_max(uint32_t n, const uint32_t *__restrict__ sid,
+                                                    const uint64_t *__restrict__ in_off,
+                                                    const uint32_t *__restrict__ wire_len,
+                                                    const uint8_t *__restrict__ in, uint32_t max_sessions,
+                                                    unsigned long long *__restrict__ smax)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t L = wire_len[i], s = sid[i];
+    if (s >= max_sessions || L < 33u)
+        return;
+    uint32_t h[16];
+    load_window(in + in_off[i], 16, h);
+    if (L <= (h[0] & 0xffu) || h[0] != 0x53454d07u || h[1] != 0x45474153u)
+        return;
+    const unsigned long long v = ((unsigned long long) bswap32(h[2]) << 32) | bswap32(h[3]);
+    if (v)
+        atomicMax(smax + s, v);
+}
+
+// ---------------------------------------------------------------- replay tables
+// The exclusive max of header-valid nonces per session in batch order (the
+// excl[] k_fixup and the body finisher read), for up to kReplayMaxSessions
+// sessions, without sorting the batch (a 16 Mi-frame radix sort + segmented
+// scan cost 1.1 ms):
+//   k_replay_tiles    tile t of the batch (T frames): per-session maxima in an
+//                     LDS table (ds_max_u64), written as row t of tab[tiles][S]
+//   k_replay_colblk   per session and block of kReplayRB rows: the block max
+//   k_replay_colscan  per session and row block: tab[t][s] := the exclusive
+//                     max over rows < t (the prefix of the block maxima, then
+//                     down the block); the last block also writes the
+//                     session's new peer nonce and session max
+//   k_replay_frames   one wave per tile walks its frames 64 at a time with the
+//                     tile's prefix row in LDS: excl = table[sid] (plus, when
+//                     a session repeats within the 64, the max of its earlier
+//                     lanes), then table[sid] = max(table[sid], v)
+constexpr uint32_t kReplayMaxSessions = 8192, kReplayRB = 64, kReplayMaxTiles = 4096;
+
+__global__ __launch_bounds__(256) void k_replay_tiles(uint32_t n, uint32_t T, uint32_t S,
+                                                     const uint32_t *__restrict__ sid,
+                                                     const unsigned long long *__restrict__ vout,
+                                                     unsigned long long *__restrict__ tab)
+{
+    extern __shared__ unsigned long long sh_tab[];
+    for (uint32_t k = threadIdx.x; k < S; k += 256)
+        sh_tab[k] = 0;
+    __syncthreads();
+    const uint64_t b = (uint64_t) blockIdx.x * T, e = b + T < n ? b + T : n;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 256) {
+        const unsigned long long v = vout[i];
+        const uint32_t s = sid[i];
+        if (v && s < S)
+            atomicMax(sh_tab + s, v);
+    }
+    __syncthreads();
+    unsigned long long *row = tab + (size_t) blockIdx.x * S;
+    for (uint32_t k = threadIdx.x; k < S; k += 256)
+        row[k] = sh_tab[k];
+}
+
+__global__ __launch_bounds__(256) void k_replay_colblk(uint32_t tiles, uint32_t S,
+                                                      const unsigned long long *__restrict__ tab,
+                                                      unsigned long long *__restrict__ blk)
+{
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x, rb = blockIdx.y;
+    if (s >= S)
+        return;
+    const uint32_t r0 = rb * kReplayRB, r1 = r0 + kReplayRB < tiles ? r0 + kReplayRB : tiles;
+    unsigned long long m = 0;
+    for (uint32_t r = r0; r < r1; ++r) {
+        const unsigned long long x = tab[(size_t) r * S + s];
+        m = x > m ? x : m;
+    }
+    blk[(size_t) rb * S + s] = m;
+}
+
+__global__ __launch_bounds__(256) void k_replay_colscan(uint32_t tiles, uint32_t S,
+                                                       unsigned long long *__restrict__ tab,
+                                                       const unsigned long long *__restrict__ blk,
+                                                       unsigned long long *__restrict__ peer,
+                                                       unsigned long long *__restrict__ smax)
+{
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x, rb = blockIdx.y;
+    if (s >= S)
+        return;
+    unsigned long long m = 0;
+    for (uint32_t k = 0; k < rb; ++k) {
+        const unsigned long long x = blk[(size_t) k * S + s];
+        m = x > m ? x : m;
+    }
+    const uint32_t r0 = rb * kReplayRB, r1 = r0 + kReplayRB < tiles ? r0 + kReplayRB : tiles;
+    for (uint32_t r = r0; r < r1; ++r) {
+        unsigned long long *p = tab + (size_t) r * S + s;
+        const unsigned long long x = *p;
+        *p = m;
+        m = x > m ? x : m;
+    }
+    if (r1 == tiles) { // the session's batch total
+        if (m > peer[s])
+            peer[s] = m;
+        if (smax)
+            smax[s] = m;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_replay_frames(uint32_t n, uint32_t T, uint32_t S,
+                                                     const uint32_t *__restrict__ sid,
+                                                     const unsigned long long *__restrict__ vout,
+                                                     const unsigned long long *__restrict__ tab,
+                                                     unsigned long long *__restrict__ excl)
+{
+    extern __shared__ unsigned long long sh_tab[]; // [S] running maxima, then [S] u32 lane tags
+    uint32_t *const tag = (uint32_t *) (sh_tab + S);
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long *row = tab + (size_t) blockIdx.x * S;
+    for (uint32_t k = lane; k < S; k += 64)
+        sh_tab[k] = row[k];
+    __syncthreads();
+    const uint64_t b = (uint64_t) blockIdx.x * T, e = b + T < n ? b + T : n;
+    for (uint64_t i0 = b; i0 < e; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const bool ok = i < e;
+        const uint32_t s = ok ? sid[i] : S;
+        const unsigned long long v = ok ? vout[i] : 0ull;
+        const bool in = ok && s < S;
+        unsigned long long x = in ? sh_tab[s] : 0ull;
+        // a session twice among these 64 frames: its earlier lanes count too
+        if (in)
+            tag[s] = lane;
+        __builtin_amdgcn_wave_barrier();
+        const bool dup = in && tag[s] != lane;
+        if (__builtin_amdgcn_ballot_w64(dup) != 0) {
+            for (uint32_t d = 1; d < 64; ++d) {
+                const uint32_t sj = __shfl_up(s, d);
+                const unsigned long long vj = __shfl_up(v, d);
+                if (lane >= d && in && sj == s && vj > x)
+                    x = vj;
+            }
+        }
+        if (ok)
+            excl[i] = x;
+        __builtin_amdgcn_wave_barrier();
+        if (in && v)
+            atomicMax(sh_tab + s, v);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -966,39 +1136,131 @@ __device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t
     }
 }
 
-// Decode: zero-fill the payload region of every big frame that failed (the
-// finishers listed them in fail_list).  A failed frame's tiles may have left
-// plaintext dirty in other XCDs' L2s, to be written back at any time, so the
-// zeroing waits for all of them: each workgroup releases its stores once at
-// its end (one L2 write-back per workgroup, not per tile) and counts itself;
-// the last one acquires, clears the listed frames and resets the counters.
-__device__ void zero_failed_frames(ZState *zs, const uint32_t *__restrict__ fail_list,
-                                   const FrameFin *__restrict__ fin, const FrameHot *__restrict__ hot)
+// ---------------------------------------------------------------- post
+// Decode, after the body kernel: the post list's zero fills and in-place
+// moves, spread over the whole grid.  An entry of len bytes is cut into
+// segments (64 KiB, or len/kPostSegs for longer moves) and segment j of
+// entry e goes to workgroup (j + e) mod grid, so one long entry uses the
+// whole chip and many short ones spread out.
+//
+// Move (dst = src - 33, overlapping): a segment reads its source in 4 KiB
+// rounds in ascending order and writes each round after the whole workgroup
+// has read it, so it only overwrites bytes it has read itself -- except that
+// its first 33 destination bytes are the previous segment's last 33 source
+// bytes, which another workgroup may not have read yet.  Those 33 bytes are
+// saved to the frame's scratch (the body's power table, dead by now) and
+// written by the last workgroup to finish.
+constexpr uint32_t kPostSeg = 64 * 1024, kPostSegs = 12, kPostRound = 4096;
+static_assert(kPostSegs * 36 <= kMaxPow * 5 * 4, "seam bytes fit the frame's power-table entry");
+
+__device__ __forceinline__ uint64_t post_seg_len(const PostOp &o)
 {
-    __shared__ uint32_t sh_nf;
+    if (o.kind != kPostMove)
+        return kPostSeg;
+    const uint64_t per = (o.len + kPostSegs - 1) / kPostSegs;
+    const uint64_t r = (per + kPostRound - 1) / kPostRound * kPostRound;
+    return r > kPostSeg ? r : kPostSeg;
+}
+
+// Workgroup zero fill of [p, p+len): dwordx4 stores, byte edges.
+__device__ void wg_zero(uint8_t *p, uint64_t len)
+{
+    const uint64_t a = (uint64_t) (uintptr_t) p, e = a + len;
+    const uint64_t a16 = (a + 15) & ~15ull, e16 = e & ~15ull;
+    if (a16 >= e16) {
+        for (uint64_t x = a + threadIdx.x; x < e; x += blockDim.x)
+            *(GU8 *) (uintptr_t) x = 0;
+        return;
+    }
+    if (threadIdx.x < a16 - a)
+        *(GU8 *) (uintptr_t) (a + threadIdx.x) = 0;
+    if (threadIdx.x < e - e16)
+        *(GU8 *) (uintptr_t) (e16 + threadIdx.x) = 0;
+    const u32x4 z = {0, 0, 0, 0};
+    for (uint64_t x = a16 + 16ull * threadIdx.x; x < e16; x += 16ull * blockDim.x)
+        *(GU4 *) (uintptr_t) x = z;
+}
+
+// Destination bytes [d0, d1) of a move by 33 (source = destination + 33),
+// ascending 4 KiB rounds, each read by the workgroup before it writes.
+__device__ void wg_move33(uint64_t d0, uint64_t d1)
+{
+    for (uint64_t r0 = d0; r0 < d1; r0 += kPostRound) {
+        const uint64_t r1 = r0 + kPostRound < d1 ? r0 + kPostRound : d1;
+        // thread t: destination bytes [r0 + 16t, +16) of the round
+        const uint64_t x = r0 + 16ull * threadIdx.x;
+        uint8_t b[16];
+        const uint32_t nb = x < r1 ? (uint32_t) (r1 - x < 16 ? r1 - x : 16) : 0u;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            b[k] = (uint32_t) k < nb ? *(const GU8 *) (uintptr_t) (x + 33 + k) : 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((uint32_t) k < nb)
+                *(GU8 *) (uintptr_t) (x + k) = b[k];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_post(ZState *__restrict__ zs, const PostOp *__restrict__ post,
+                                              uint8_t *__restrict__ seam)
+{
+    const uint32_t np = zs->post_n; // appended by the kernels before this one (stream order)
+    const uint32_t G = gridDim.x;
+    for (uint32_t e = 0; e < np; ++e) {
+        const PostOp o = post[e];
+        const uint64_t seg = post_seg_len(o);
+        const uint64_t nseg = (o.len + seg - 1) / seg;
+        for (uint64_t j = (blockIdx.x + G - e % G) % G; j < nseg; j += G) {
+            const uint64_t a = j * seg, b = a + seg < o.len ? a + seg : o.len;
+            if (o.kind == kPostZero) {
+                wg_zero((uint8_t *) (uintptr_t) (o.dst + a), b - a);
+            } else {
+                // segment j > 0: its first 33 destination bytes wait for the seam pass
+                uint64_t w0 = o.dst + a;
+                if (j > 0) {
+                    const uint64_t ns = b - a < 33 ? b - a : 33;
+                    if (threadIdx.x < ns)
+                        seam[(size_t) o.p * (kMaxPow * 5 * 4) + 36 * j + threadIdx.x] =
+                            *(const GU8 *) (uintptr_t) (w0 + 33 + threadIdx.x);
+                    __syncthreads();
+                    w0 += ns;
+                }
+                wg_move33(w0, o.dst + b);
+            }
+        }
+    }
+    // the last workgroup: the seams (every segment has read its source), reset
+    __shared__ uint32_t sh_last;
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t d = __hip_atomic_fetch_add(&zs->body_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh_nf = 0xffffffffu;
-        if (d + 1u == gridDim.x) {
+        const uint32_t d = __hip_atomic_fetch_add(&zs->post_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_last = d + 1u == G;
+        if (sh_last)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            sh_nf = __hip_atomic_load(&zs->body_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->body_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->body_fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!sh_last)
+        return;
+    for (uint32_t e = 0; e < np; ++e) {
+        const PostOp o = post[e];
+        if (o.kind != kPostMove)
+            continue;
+        const uint64_t seg = post_seg_len(o);
+        const uint64_t nseg = (o.len + seg - 1) / seg;
+        for (uint64_t t = threadIdx.x; t < (nseg - 1) * 36; t += blockDim.x) {
+            const uint64_t j = 1 + t / 36, k = t % 36;
+            const uint64_t a = j * seg;
+            if (k < 33 && a + k < o.len)
+                *(GU8 *) (uintptr_t) (o.dst + a + k) = seam[(size_t) o.p * (kMaxPow * 5 * 4) + 36 * j + k];
         }
     }
     __syncthreads();
-    const uint32_t nf = sh_nf;
-    if (nf == 0xffffffffu)
-        return;
-    for (uint32_t f = 0; f < nf; ++f) {
-        const uint32_t q = fail_list[f];
-        uint8_t *o = (uint8_t *) (uintptr_t) hot[q].out_base;
-        const uint32_t len = fin[q].wire_len - 33u;
-        for (uint32_t b = threadIdx.x; b < len; b += kBodyThreads)
-            o[b] = 0;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&zs->post_n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zs->post_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1010,7 +1272,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
     const FrameHot *__restrict__ hot, const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
     const uint32_t *__restrict__ powtab, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
     unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
-    const unsigned long long *__restrict__ psnap, uint32_t *__restrict__ fail_list)
+    const unsigned long long *__restrict__ psnap, PostOp *__restrict__ post)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kBufLds];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1221,11 +1483,17 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
                                            : diff              ? ZMQG_ERR_CRYPTOGRAPHIC // :277-281
                                                                : 0;
                     status_out[i] = status;
-                    flags_out[i] = status == 0 ? (uint8_t) cur.flags : 0;
-                    if (status != 0) // its payload region is zero-filled at the kernel's end
-                        fail_list[__hip_atomic_fetch_add(&zs->body_fail, 1u, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)] = p;
-                    (void) wire_len;
+                    flags_out[i] = status == 0 ? (uint8_t) (cur.flags & 3u) : 0;
+                    // k_post, after every tile of this call: a failed frame's
+                    // region is zero-filled (its tiles' plaintext may still sit
+                    // dirty in other XCDs' L2s, so not here), an in-place frame
+                    // moved to the frame's start
+                    const bool mv = (cur.flags & kHotMove) != 0;
+                    if (status != 0)
+                        post_append(zs, post, cur.out_base - (mv ? 33u : 0u), mv ? wire_len : wire_len - 33u,
+                                    kPostZero, p);
+                    else if (mv)
+                        post_append(zs, post, cur.out_base - 33u, wire_len - 33u, kPostMove, p);
                 }
             }
         }
@@ -1241,9 +1509,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         cur = nx;
         lkn = lk2;
     }
-    } // tb < te (waves without tiles still take part in the decode zero-fill)
-    if (DEC)
-        zero_failed_frames(zs, fail_list, fin, hot);
+    } // tb < te
 }
 
 } // namespace
@@ -1254,16 +1520,28 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
 namespace {
 
 template <typename T>
-int grow(zmqg_ctx *ctx, T *&p, size_t count)
+int grow(zmqg_ctx *ctx, T *&p, size_t count, hipStream_t st)
 {
     if (p)
-        ZCHECK(ctx, hipFree(p));
+        ZCHECK(ctx, hipFreeAsync(p, st));
     p = nullptr;
-    ZCHECK(ctx, hipMalloc((void **) &p, count * sizeof(T) + 64));
+    ZCHECK(ctx, hipMallocAsync((void **) &p, count * sizeof(T) + 64, st));
     return 0;
 }
 
-int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
+__global__ void k_zstate_init(ZState *zs)
+{
+    if (threadIdx.x == 0) {
+        ZState z{};
+        z.epoch = 1;
+        *zs = z;
+    }
+}
+
+// Workspace for n frames, grown in stream order on the batch's stream: the
+// old buffers are freed and the new ones allocated and initialised on `st`,
+// after the work already queued there (no device-wide synchronisation).
+int ensure_workspace(zmqg_ctx *ctx, uint64_t n, hipStream_t st)
 {
     Workspace &w = ctx->ws;
     if (n > w.cap) {
@@ -1271,34 +1549,29 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
         while (cap < n)
             cap *= 2;
         int rc;
-        if ((rc = grow(ctx, w.hot, cap)) || (rc = grow(ctx, w.pw, cap)) || (rc = grow(ctx, w.fin, cap)) ||
-            (rc = grow(ctx, w.powtab, cap * kMaxPow * 5)) ||
-            (rc = grow(ctx, w.acc, cap * 5)) || (rc = grow(ctx, w.cnt, cap)) || (rc = grow(ctx, w.nch, cap)) ||
-            (rc = grow(ctx, w.chunk_end, cap)) || (rc = grow(ctx, w.v, cap)) || (rc = grow(ctx, w.excl, cap)) ||
-            (rc = grow(ctx, w.v_s, cap)) || (rc = grow(ctx, w.excl_s, cap)) || (rc = grow(ctx, w.iota, cap)) ||
-            (rc = grow(ctx, w.perm, cap)) || (rc = grow(ctx, w.keys_s, cap)) || (rc = grow(ctx, w.last, cap)) ||
-            (rc = grow(ctx, w.list_frame, cap)) || (rc = grow(ctx, w.fail, cap)) || (rc = grow(ctx, w.psnap, cap)) ||
-            (rc = grow(ctx, w.blockmax, cap)) || (rc = grow(ctx, w.lb_flag, cap)) || (rc = grow(ctx, w.lb_agg, cap)) ||
-            (rc = grow(ctx, w.lb_inc, cap)))
+        if ((rc = grow(ctx, w.hot, cap, st)) || (rc = grow(ctx, w.pw, cap, st)) || (rc = grow(ctx, w.fin, cap, st)) ||
+            (rc = grow(ctx, w.powtab, cap * kMaxPow * 5, st)) ||
+            (rc = grow(ctx, w.acc, cap * 5, st)) || (rc = grow(ctx, w.cnt, cap, st)) || (rc = grow(ctx, w.nch, cap, st)) ||
+            (rc = grow(ctx, w.chunk_end, cap, st)) || (rc = grow(ctx, w.v, cap, st)) || (rc = grow(ctx, w.excl, cap, st)) ||
+            (rc = grow(ctx, w.v_s, cap, st)) || (rc = grow(ctx, w.excl_s, cap, st)) || (rc = grow(ctx, w.iota, cap, st)) ||
+            (rc = grow(ctx, w.perm, cap, st)) || (rc = grow(ctx, w.keys_s, cap, st)) || (rc = grow(ctx, w.last, cap, st)) ||
+            (rc = grow(ctx, w.list_frame, cap, st)) || (rc = grow(ctx, w.post, cap, st)) ||
+            (rc = grow(ctx, w.psnap, cap, st)) || (rc = grow(ctx, w.blockmax, cap, st)) ||
+            (rc = grow(ctx, w.lb_flag, cap, st)) || (rc = grow(ctx, w.lb_agg, cap, st)) || (rc = grow(ctx, w.lb_inc, cap, st)))
             return rc;
-        ZCHECK(ctx, hipMemset(w.lb_flag, 0, cap * sizeof(unsigned long long)));
+        ZCHECK(ctx, hipMemsetAsync(w.lb_flag, 0, cap * sizeof(unsigned long long), st));
         if (!w.zs) {
-            if ((rc = grow(ctx, w.zs, 1)))
+            if ((rc = grow(ctx, w.zs, 1, st)))
                 return rc;
-            ZState z0{};
-            z0.epoch = 1;
-            ZCHECK(ctx, hipMemcpy(w.zs, &z0, sizeof z0, hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(k_zstate_init, dim3(1), dim3(64), 0, st, w.zs);
+            ZCHECK(ctx, hipGetLastError());
         }
-        // hipMemset / hipMemcpy run on the null stream and may still be in
-        // flight when they return; the batch's kernels run on the caller's
-        // stream (possibly non-blocking), so wait for them here (growth only)
-        ZCHECK(ctx, hipDeviceSynchronize());
         w.cap = cap;
     }
     // hipCUB temporaries for n frames
     size_t need = 0, b = 0;
     const int nn = (int) n;
-    if (ctx->sort_bits > 0) {
+    if (ctx->sort_bits > 0 && ctx->max_sessions > kReplayMaxSessions) { // the sort fallback of replay_multi
         b = 0;
         ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t *) nullptr, w.keys_s,
                                                         (const uint32_t *) nullptr, w.perm, nn, 0, ctx->sort_bits));
@@ -1313,9 +1586,9 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n)
         while (cap < need)
             cap *= 2;
         if (w.temp)
-            ZCHECK(ctx, hipFree(w.temp));
+            ZCHECK(ctx, hipFreeAsync(w.temp, st));
         w.temp = nullptr;
-        ZCHECK(ctx, hipMalloc(&w.temp, cap));
+        ZCHECK(ctx, hipMallocAsync(&w.temp, cap, st));
         w.temp_bytes = cap;
     }
     return 0;
@@ -1403,17 +1676,19 @@ template <bool DEC, class BigOp>
 void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const uint64_t *nonce,
                    const uint8_t *flags, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
                    const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
-                   uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs)
+                   uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs, FrameCtl ctl)
 {
     const dim3 grid((uint32_t) (((uint64_t) n * (G ? G : 1) + kFramesBS - 1) / kFramesBS));
     if (G == 0) {
         hipLaunchKernelGGL((k_frames_seq<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
-                           out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs);
+                           out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
+                           ctl);
         return;
     }
 #define ZMQG_LAUNCH_FRAMES(GG)                                                                                        \
     hipLaunchKernelGGL((k_frames<DEC, GG, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,      \
-                       out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs)
+                       out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs, \
+                       ctl)
     if (G == 1)
         ZMQG_LAUNCH_FRAMES(1);
     else if (G == 2)
@@ -1421,6 +1696,59 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
     else
         ZMQG_LAUNCH_FRAMES(4);
 #undef ZMQG_LAUNCH_FRAMES
+}
+
+// Multi-session replay prefix (k_fixup's excl) after the frame kernel: the
+// replay tables for up to kReplayMaxSessions sessions, else sort by session +
+// segmented scan (hipCUB).  Writes each session's new peer nonce (and its
+// batch max into smax when given).
+int replay_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st, unsigned long long *smax)
+{
+    Workspace &w = ctx->ws;
+    const uint32_t S = ctx->max_sessions;
+    if (S <= kReplayMaxSessions) {
+        uint32_t T = 4096;
+        while ((nn + T - 1) / T > kReplayMaxTiles)
+            T *= 2;
+        const uint32_t tiles = (nn + T - 1) / T, rbs = (tiles + kReplayRB - 1) / kReplayRB;
+        const size_t need = ((size_t) tiles + rbs) * S;
+        if (need > w.rt_cap) {
+            if (w.rt)
+                ZCHECK(ctx, hipFreeAsync(w.rt, st));
+            w.rt = nullptr;
+            ZCHECK(ctx, hipMallocAsync((void **) &w.rt, need * sizeof(unsigned long long), st));
+            w.rt_cap = need;
+        }
+        unsigned long long *tab = w.rt, *blk = w.rt + (size_t) tiles * S;
+        hipLaunchKernelGGL(k_replay_tiles, dim3(tiles), dim3(256), S * sizeof(unsigned long long), st, nn, T, S, sid,
+                           (const unsigned long long *) w.v, tab);
+        ZCHECK(ctx, hipGetLastError());
+        const dim3 cg((S + 255) / 256, rbs);
+        hipLaunchKernelGGL(k_replay_colblk, cg, dim3(256), 0, st, tiles, S, (const unsigned long long *) tab, blk);
+        ZCHECK(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_replay_colscan, cg, dim3(256), 0, st, tiles, S, tab, (const unsigned long long *) blk,
+                           ctx->peer, smax);
+        ZCHECK(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_replay_frames, dim3(tiles), dim3(64), S * (sizeof(unsigned long long) + 4), st, nn, T, S,
+                           sid, (const unsigned long long *) w.v, (const unsigned long long *) tab, w.excl);
+        ZCHECK(ctx, hipGetLastError());
+        w.use_last = false;
+        return 0;
+    }
+    const dim3 hgrid((nn + kHeadThreads - 1) / kHeadThreads);
+    size_t tb = w.temp_bytes;
+    ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(w.temp, tb, sid, w.keys_s, w.iota, w.perm, (int) nn, 0,
+                                                    ctx->sort_bits, st));
+    hipLaunchKernelGGL(k_gather_u64, hgrid, dim3(kHeadThreads), 0, st, nn, w.perm, w.v, w.v_s);
+    ZCHECK(ctx, hipGetLastError());
+    tb = w.temp_bytes;
+    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScanByKey(w.temp, tb, w.keys_s, w.v_s, w.excl_s, hipcub::Max(),
+                                                        0ull, (int) nn, hipcub::Equality(), st));
+    hipLaunchKernelGGL(k_scatter_replay, hgrid, dim3(kHeadThreads), 0, st, nn, w.perm, w.keys_s, w.excl_s, w.excl,
+                       w.last);
+    ZCHECK(ctx, hipGetLastError());
+    w.use_last = true;
+    return 0;
 }
 
 } // namespace
@@ -1454,23 +1782,23 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
     }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    // The tables are cleared on the ctx's own stream and that stream alone is
+    // waited for (a null-stream memset is not ordered before the non-blocking
+    // streams the batches run on: a session installed right after could be
+    // cleared by the late memset).  No device-wide synchronisation.
+    if (e == hipSuccess)
         e = hipMalloc((void **) &ctx->sessions, sizeof(DevSession) * max_sessions);
     if (e == hipSuccess)
-        e = hipMemset(ctx->sessions, 0, sizeof(DevSession) * max_sessions);
+        e = hipMemsetAsync(ctx->sessions, 0, sizeof(DevSession) * max_sessions, ctx->own_stream);
     if (e == hipSuccess)
         e = hipMalloc((void **) &ctx->peer, sizeof(unsigned long long) * max_sessions);
     if (e == hipSuccess)
-        e = hipMemset(ctx->peer, 0, sizeof(unsigned long long) * max_sessions);
-    // the memsets are queued on the null stream, which the ctx's non-blocking
-    // stream does not wait for: without this, a session installed right after
-    // could be zeroed by the late memset (seen as every MAC failing on the
-    // first context of a fresh process)
+        e = hipMemsetAsync(ctx->peer, 0, sizeof(unsigned long long) * max_sessions, ctx->own_stream);
     if (e == hipSuccess)
-        e = hipDeviceSynchronize();
+        e = hipStreamSynchronize(ctx->own_stream);
     if (e == hipSuccess)
         e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         fprintf(stderr, "zmqg_ctx_create: %s\n", hipGetErrorString(e));
         zmqg_ctx_destroy(ctx);
@@ -1485,11 +1813,15 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     if (!ctx)
         return -EINVAL;
     (void) hipSetDevice(ctx->device);
-    (void) hipDeviceSynchronize();
+    // the ctx's work is on its last batch stream and its own stream
+    if (ctx->last_stream)
+        (void) hipStreamSynchronize(ctx->last_stream);
+    if (ctx->own_stream)
+        (void) hipStreamSynchronize(ctx->own_stream);
     Workspace &w = ctx->ws;
     void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
-                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.fail, w.psnap, w.blockmax, w.zs,
-                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, ctx->sessions, ctx->peer, ctx->dbuf};
+                    w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.post, w.psnap, w.blockmax, w.zs,
+                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, w.rt, ctx->sessions, ctx->peer, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
             (void) hipFree(p);
@@ -1533,10 +1865,10 @@ int zmqg_ctx_get_profile(zmqg_ctx *ctx, int kind, double *ms_total, uint64_t *la
     if (!ctx || kind < 0 || kind > 5 || !ms_total || !launches)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    ZCHECK(ctx, hipDeviceSynchronize());
     double tot = 0;
     for (auto &p : ctx->prof[kind]) {
         float ms = 0;
+        ZCHECK(ctx, hipEventSynchronize(p.second));
         ZCHECK(ctx, hipEventElapsedTime(&ms, p.first, p.second));
         tot += ms;
         ctx->event_pool.push_back(p.first);
@@ -1609,11 +1941,11 @@ int zmqg_session_set_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t peer_nonce
     if (!ctx || sid >= ctx->max_sessions)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    ZCHECK(ctx, hipDeviceSynchronize());
-    hipLaunchKernelGGL(k_set_peer, dim3(1), dim3(64), 0, ctx->own_stream, ctx->peer, sid,
-                       (unsigned long long) peer_nonce);
+    // in order after the batches already issued (on the ctx's last batch stream)
+    hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->own_stream;
+    hipLaunchKernelGGL(k_set_peer, dim3(1), dim3(64), 0, st, ctx->peer, sid, (unsigned long long) peer_nonce);
     ZCHECK(ctx, hipGetLastError());
-    ZCHECK(ctx, hipStreamSynchronize(ctx->own_stream));
+    ZCHECK(ctx, hipStreamSynchronize(st));
     return 0;
 }
 
@@ -1622,9 +1954,10 @@ int zmqg_session_get_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *peer_nonc
     if (!ctx || sid >= ctx->max_sessions || !peer_nonce_out)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    ZCHECK(ctx, hipDeviceSynchronize());
+    hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->own_stream;
     unsigned long long v = 0;
-    ZCHECK(ctx, hipMemcpy(&v, ctx->peer + sid, sizeof v, hipMemcpyDeviceToHost));
+    ZCHECK(ctx, hipMemcpyAsync(&v, ctx->peer + sid, sizeof v, hipMemcpyDeviceToHost, st));
+    ZCHECK(ctx, hipStreamSynchronize(st));
     *peer_nonce_out = v;
     return 0;
 }
@@ -1638,11 +1971,16 @@ uint64_t zmqg_wire_size(uint8_t msg_flags, int downgrade_sub, uint64_t payload_l
     return 32 + hl + payload_len;
 }
 
-int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
-                      const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
-                      uint8_t *out, void *stream)
+static int check_opts(const zmqg_batch_opts *o)
 {
-    if (!ctx || check_n(n))
+    return o && o->size < sizeof(zmqg_batch_opts) ? -EINVAL : 0;
+}
+
+int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                         const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                         uint8_t *out, const zmqg_batch_opts *opts, void *stream)
+{
+    if (!ctx || check_n(n) || check_opts(opts))
         return -EINVAL;
     if (n == 0)
         return 0;
@@ -1650,12 +1988,20 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         return -EINVAL;
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    int rc = ensure_workspace(ctx, n);
+    ctx->last_stream = st;
+    int rc = ensure_workspace(ctx, n, st);
     if (rc)
         return rc;
     Workspace &w = ctx->ws;
     const uint32_t nn = (uint32_t) n;
     const int G = lanes_per_frame(ctx, nn);
+    FrameCtl ctl{};
+    if (opts) {
+        ctl.enc_status = opts->status_out;
+        ctl.max_len = opts->max_len;
+        // every frame within the bound fits the frame kernel: no body launch
+        ctl.no_body = opts->max_len && opts->max_len + 43u <= kMaxFrameStream;
+    }
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_ENCODE_MAIN, st);
@@ -1663,25 +2009,34 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
                          ctx->max_sessions, nullptr, nullptr, ReplayOut{},
                          EncodeHead{sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
                                     ctx->max_sessions, R},
-                         w.zs);
+                         w.zs, ctl);
     ZCHECK(ctx, hipGetLastError());
     main.end();
-    ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
-    hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
-                       w.pw, w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, w.acc, w.cnt,
-                       (const unsigned long long *) nullptr, (const unsigned long long *) nullptr,
-                       (uint32_t *) nullptr);
-    ZCHECK(ctx, hipGetLastError());
-    body.end();
+    if (!ctl.no_body) {
+        ProfSpan body(ctx, ZMQG_PROF_ENCODE_BODY, st);
+        hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
+                           w.pw, w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, w.acc, w.cnt,
+                           (const unsigned long long *) nullptr, (const unsigned long long *) nullptr,
+                           (PostOp *) nullptr);
+        ZCHECK(ctx, hipGetLastError());
+        body.end();
+    }
     call.end();
     return 0;
 }
 
-int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
-                      const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
-                      uint8_t *flags_out, int32_t *status_out, void *stream)
+int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                      const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                      uint8_t *out, void *stream)
 {
-    if (!ctx || check_n(n))
+    return zmqg_encode_batch_ex(ctx, n, sid, nonce, flags, in_off, len, in, out_off, out, nullptr, stream);
+}
+
+int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                         const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
+                         uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts, void *stream)
+{
+    if (!ctx || check_n(n) || check_opts(opts))
         return -EINVAL;
     if (n == 0)
         return 0;
@@ -1689,14 +2044,22 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
         return -EINVAL;
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    int rc = ensure_workspace(ctx, n);
+    ctx->last_stream = st;
+    int rc = ensure_workspace(ctx, n, st);
     if (rc)
         return rc;
     Workspace &w = ctx->ws;
     const uint32_t nn = (uint32_t) n;
-    const dim3 hgrid((nn + kHeadThreads - 1) / kHeadThreads);
     const int G = lanes_per_frame(ctx, nn);
     const bool multi = ctx->sort_bits > 0;
+    FrameCtl ctl{};
+    ctl.post = w.post;
+    unsigned long long *smax = nullptr;
+    if (opts) {
+        ctl.max_len = opts->max_len;
+        ctl.no_body = opts->max_len && opts->max_len <= kMaxFrameStream;
+        smax = (unsigned long long *) opts->session_max_out;
+    }
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ReplayOut rp{};
     rp.vout = w.v;
@@ -1704,11 +2067,14 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     rp.peer = ctx->peer;
     if (multi) {
         rp.iota = w.iota;
+        if (smax)
+            ZCHECK(ctx, hipMemsetAsync(smax, 0, sizeof(unsigned long long) * ctx->max_sessions, st));
     } else {
         rp.excl = w.excl;
         rp.lb_flag = w.lb_flag;
         rp.lb_agg = w.lb_agg;
         rp.lb_inc = w.lb_inc;
+        rp.smax = smax;
         // A grid that fits the device at once can use blockIdx as the
         // look-back order (every workgroup becomes resident eventually,
         // whatever the dispatch order); a larger one takes tickets.
@@ -1720,34 +2086,54 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     launch_frames<true>(G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out, ctx->sessions,
                         ctx->max_sessions, flags_out, status_out, rp,
                         DecodeHead{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R},
-                        w.zs);
+                        w.zs, ctl);
     ZCHECK(ctx, hipGetLastError());
     main.end();
-    if (multi) {
-        size_t tb = w.temp_bytes;
-        ZCHECK(ctx, hipcub::DeviceRadixSort::SortPairs(w.temp, tb, sid, w.keys_s, w.iota, w.perm, (int) nn, 0,
-                                                        ctx->sort_bits, st));
-        hipLaunchKernelGGL(k_gather_u64, hgrid, dim3(kHeadThreads), 0, st, nn, w.perm, w.v, w.v_s);
+    if (multi && (rc = replay_multi(ctx, nn, sid, st, smax)))
+        return rc;
+    if (!ctl.no_body) {
+        ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
+        hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
+                           w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap, w.post);
         ZCHECK(ctx, hipGetLastError());
-        tb = w.temp_bytes;
-        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveScanByKey(w.temp, tb, w.keys_s, w.v_s, w.excl_s, hipcub::Max(),
-                                                            0ull, (int) nn, hipcub::Equality(), st));
-        hipLaunchKernelGGL(k_scatter_replay, hgrid, dim3(kHeadThreads), 0, st, nn, w.perm, w.keys_s, w.excl_s, w.excl,
-                           w.last);
+        hipLaunchKernelGGL(k_post, dim3(body_grid(ctx)), dim3(256), 0, st, w.zs, (const PostOp *) w.post,
+                           (uint8_t *) w.powtab);
         ZCHECK(ctx, hipGetLastError());
+        body.end();
     }
-    ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
-    hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
-                       w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap, w.fail);
-    ZCHECK(ctx, hipGetLastError());
-    body.end();
     if (multi) {
         hipLaunchKernelGGL(k_fixup, dim3((nn + kFixupThreads - 1) / kFixupThreads), dim3(kFixupThreads), 0, st, nn,
-                           kMaxFrameStream, w.v, w.psnap, w.excl, w.last, sid, ctx->max_sessions, wire_len, out_off,
-                           out, status_out, flags_out, ctx->peer);
+                           kMaxFrameStream, w.v, w.psnap, w.excl, w.use_last ? w.last : nullptr, sid,
+                           ctx->max_sessions, wire_len, out_off, out, status_out, flags_out, ctx->peer, smax);
         ZCHECK(ctx, hipGetLastError());
     }
     call.end();
+    return 0;
+}
+
+int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                      const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
+                      uint8_t *flags_out, int32_t *status_out, void *stream)
+{
+    return zmqg_decode_batch_ex(ctx, n, sid, in_off, wire_len, in, out_off, out, flags_out, status_out, nullptr,
+                                stream);
+}
+
+int zmqg_session_max_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                           const uint32_t *wire_len, const uint8_t *in, uint64_t *session_max_out, void *stream)
+{
+    if (!ctx || check_n(n) || !session_max_out)
+        return -EINVAL;
+    if (n > 0 && (!sid || !in_off || !wire_len || !in))
+        return -EINVAL;
+    hipStream_t st = (hipStream_t) stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    ZCHECK(ctx, hipMemsetAsync(session_max_out, 0, sizeof(uint64_t) * ctx->max_sessions, st));
+    if (n == 0)
+        return 0;
+    hipLaunchKernelGGL(k_session_max, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, st, (uint32_t) n, sid, in_off,
+                       wire_len, in, ctx->max_sessions, (unsigned long long *) session_max_out);
+    ZCHECK(ctx, hipGetLastError());
     return 0;
 }
 
@@ -1868,7 +2254,7 @@ int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     return 0;
 }
 
-static int zmtp_temp(zmqg_ctx *ctx, size_t need)
+static int zmtp_temp(zmqg_ctx *ctx, size_t need, hipStream_t st)
 {
     ZmtpWs &z = ctx->zw;
     if (need <= z.temp_bytes)
@@ -1877,10 +2263,10 @@ static int zmtp_temp(zmqg_ctx *ctx, size_t need)
     while (cap < need)
         cap *= 2;
     if (z.temp)
-        ZCHECK(ctx, hipFree(z.temp));
+        ZCHECK(ctx, hipFreeAsync(z.temp, st));
     z.temp = nullptr;
     z.temp_bytes = 0;
-    ZCHECK(ctx, hipMalloc(&z.temp, cap));
+    ZCHECK(ctx, hipMallocAsync(&z.temp, cap, st));
     z.temp_bytes = cap;
     return 0;
 }
@@ -1905,13 +2291,13 @@ int zmqg_encode_zmtp(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
         uint64_t cap = z.n_cap ? z.n_cap : 1024;
         while (cap < n)
             cap *= 2;
-        if ((rc = grow(ctx, z.F, cap + 1)) || (rc = grow(ctx, z.wire_off, cap)))
+        if ((rc = grow(ctx, z.F, cap + 1, st)) || (rc = grow(ctx, z.wire_off, cap, st)))
             return rc;
         z.n_cap = cap;
     }
     size_t need = 0;
     ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.F, frame_off, (int) (n + 1), st));
-    if ((rc = zmtp_temp(ctx, need)))
+    if ((rc = zmtp_temp(ctx, need, st)))
         return rc;
     const unsigned g1 = (unsigned) ((n + 1 + 255) / 256), g0 = (unsigned) ((n + 255) / 256);
     hipLaunchKernelGGL(k_zmtp_sizes, dim3(g1), dim3(256), 0, st, n, sid, flags, len, ctx->sessions,
@@ -1946,7 +2332,7 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
         uint64_t cap = z.c_cap ? z.c_cap : 1024;
         while (cap < ccap)
             cap *= 2;
-        if ((rc = grow(ctx, z.cand, cap)) || (rc = grow(ctx, z.bad, cap)) || (rc = grow(ctx, z.cand0, cap)))
+        if ((rc = grow(ctx, z.cand, cap, st)) || (rc = grow(ctx, z.bad, cap, st)) || (rc = grow(ctx, z.cand0, cap, st)))
             return rc;
         z.c_cap = cap;
     }
@@ -1956,14 +2342,14 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
         uint64_t cap = z.f_cap ? z.f_cap : 1024;
         while (cap < fcap)
             cap *= 2;
-        if ((rc = grow(ctx, z.run, 2 * cap)) || (rc = grow(ctx, z.runpre, cap)) || (rc = grow(ctx, z.psize, cap + 1)) ||
-            (rc = grow(ctx, z.poff, cap + 1)) || (rc = grow(ctx, z.sid_fill, cap)) || (rc = grow(ctx, z.fflags, cap)))
+        if ((rc = grow(ctx, z.run, 2 * cap, st)) || (rc = grow(ctx, z.runpre, cap, st)) || (rc = grow(ctx, z.psize, cap + 1, st)) ||
+            (rc = grow(ctx, z.poff, cap + 1, st)) || (rc = grow(ctx, z.sid_fill, cap, st)) || (rc = grow(ctx, z.fflags, cap, st)))
             return rc;
         z.f_cap = cap;
     }
-    if (!z.counts && (rc = grow(ctx, z.counts, 3)))
+    if (!z.counts && (rc = grow(ctx, z.counts, 3, st)))
         return rc;
-    if (!z.walk && (rc = grow(ctx, z.walk, 1)))
+    if (!z.walk && (rc = grow(ctx, z.walk, 1, st)))
         return rc;
     hipcub::CountingInputIterator<uint64_t> pos(0);
     // candidates (unordered), then sorted by offset
@@ -1981,7 +2367,7 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
         while (bits < 64 && (1ull << bits) < in_bytes)
             ++bits;
         ZCHECK(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, need, z.cand0, z.cand, (int) m, 0, bits, st));
-        if ((rc = zmtp_temp(ctx, need)))
+        if ((rc = zmtp_temp(ctx, need, st)))
             return rc;
         tb = z.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceRadixSort::SortKeys(z.temp, tb, z.cand0, z.cand, (int) m, 0, bits, st));
@@ -1990,7 +2376,7 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
         const ZmtpIsUnlinked isu{in, in_bytes, z.cand, z.counts};
         need = 0;
         ZCHECK(ctx, hipcub::DeviceSelect::If(nullptr, need, pos, z.bad, z.counts + 1, (int) m, isu, st));
-        if ((rc = zmtp_temp(ctx, need)))
+        if ((rc = zmtp_temp(ctx, need, st)))
             return rc;
         tb = z.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceSelect::If(z.temp, tb, pos, z.bad, z.counts + 1, (int) m, isu, st));
@@ -2018,7 +2404,7 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
     ZCHECK(ctx, hipGetLastError());
     need = 0;
     ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.psize, z.poff, (int) (nf + 1), st));
-    if ((rc = zmtp_temp(ctx, need)))
+    if ((rc = zmtp_temp(ctx, need, st)))
         return rc;
     tb = z.temp_bytes;
     ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.psize, z.poff, (int) (nf + 1), st));

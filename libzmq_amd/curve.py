@@ -29,6 +29,12 @@ ERR_INVALID_SEQUENCE = 0x10000002
 ERR_MALFORMED_UNSPECIFIED = 0x10000011
 ERR_MALFORMED_MESSAGE = 0x10000012
 ERR_CRYPTOGRAPHIC = 0x11000001
+# library codes (zmqg_curve.h): unknown session; frame above the caller's max_len
+ERR_SESSION = 0x7A000001
+ERR_BOUND = 0x7A000002
+# the largest max_len for which a call skips the large-frame kernels
+MAX_LEN_FRAME_KERNEL_DECODE = 4608
+MAX_LEN_FRAME_KERNEL_ENCODE = 4565
 
 # src/msg.hpp:55-62
 MORE, COMMAND, SUBSCRIBE, CANCEL = 1, 2, 12, 16
@@ -54,6 +60,14 @@ _lib.zmqg_wire_size.argtypes = [ctypes.c_uint8, ctypes.c_int, _U64]
 _lib.zmqg_wire_size.restype = _U64
 _lib.zmqg_encode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
+class BatchOpts(ctypes.Structure):  # zmqg_batch_opts
+    _fields_ = [("size", _U32), ("reserved", _U32), ("max_len", _U64), ("status_out", _P),
+                ("session_max_out", _P)]
+
+
+_lib.zmqg_encode_batch_ex.argtypes = [_P, _U64] + [_P] * 8 + [ctypes.POINTER(BatchOpts), _P]
+_lib.zmqg_decode_batch_ex.argtypes = [_P, _U64] + [_P] * 8 + [ctypes.POINTER(BatchOpts), _P]
+_lib.zmqg_session_max_batch.argtypes = [_P, _U64] + [_P] * 6
 _lib.zmqg_encode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _U64, _P, _P, _U64]
 _lib.zmqg_decode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _U64, _P, _P, _U64, _P, _P]
 class ZmtpResult(ctypes.Structure):  # zmqg_zmtp_result
@@ -80,7 +94,7 @@ _lib.zmqg_ctx_set_profiling.argtypes = [_P, ctypes.c_int]
 _lib.zmqg_ctx_get_profile.argtypes = [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
 _lib.zmqg_last_error.argtypes = [_P]
 _lib.zmqg_last_error.restype = ctypes.c_char_p
-assert _lib.zmqg_abi_version() == 1
+assert _lib.zmqg_abi_version() == 2
 
 
 def lib():
@@ -175,17 +189,39 @@ class CurveContext:
         return ms.value, cnt.value
 
     # ---- device-resident batches (torch tensors on self.device) ----
-    def encode_batch(self, sid, nonce, flags, in_off, length, inp, out_off, out, stream=None):
-        n = int(sid.numel())
-        self._check(_lib.zmqg_encode_batch(self._ctx, n, _ptr(sid), _ptr(nonce), _ptr(flags), _ptr(in_off),
-                                           _ptr(length), _ptr(inp), _ptr(out_off), _ptr(out), _stream_handle(stream)),
-                    "zmqg_encode_batch")
+    # max_len / status_out / session_max_out: zmqg_batch_opts (the _ex calls)
+    @staticmethod
+    def _opts(max_len, status_out, session_max_out):
+        if not max_len and status_out is None and session_max_out is None:
+            return None
+        o = BatchOpts(ctypes.sizeof(BatchOpts), 0, int(max_len or 0), _ptr(status_out), _ptr(session_max_out))
+        return ctypes.byref(o), o
 
-    def decode_batch(self, sid, in_off, wire_len, inp, out_off, out, flags_out, status_out, stream=None):
+    def encode_batch(self, sid, nonce, flags, in_off, length, inp, out_off, out, stream=None, max_len=0,
+                     status_out=None):
         n = int(sid.numel())
-        self._check(_lib.zmqg_decode_batch(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
-                                           _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
-                                           _stream_handle(stream)), "zmqg_decode_batch")
+        o = self._opts(max_len, status_out, None)
+        self._check(_lib.zmqg_encode_batch_ex(self._ctx, n, _ptr(sid), _ptr(nonce), _ptr(flags), _ptr(in_off),
+                                              _ptr(length), _ptr(inp), _ptr(out_off), _ptr(out),
+                                              o[0] if o else None, _stream_handle(stream)), "zmqg_encode_batch")
+
+    def decode_batch(self, sid, in_off, wire_len, inp, out_off, out, flags_out, status_out, stream=None, max_len=0,
+                     session_max_out=None):
+        """session_max_out: int64 tensor of max_sessions entries (device),
+        receives each session's largest header-valid nonce of the batch."""
+        n = int(sid.numel())
+        o = self._opts(max_len, None, session_max_out)
+        self._check(_lib.zmqg_decode_batch_ex(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
+                                              _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
+                                              o[0] if o else None, _stream_handle(stream)), "zmqg_decode_batch")
+
+    def session_max_batch(self, sid, in_off, wire_len, inp, session_max_out, stream=None):
+        """Header pass: session_max_out (int64, max_sessions entries) = each
+        session's largest header-valid nonce among the frames (sharded decode)."""
+        n = int(sid.numel())
+        self._check(_lib.zmqg_session_max_batch(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
+                                                _ptr(session_max_out), _stream_handle(stream)),
+                    "zmqg_session_max_batch")
 
     # ---- ZMTP framing on the device (device tensors) ----
     def encode_zmtp(self, sid, nonce, flags, in_off, length, inp, out, frame_off, stream=None):

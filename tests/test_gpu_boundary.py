@@ -1,0 +1,466 @@
+"""GPU tests of the boundary's round-2 behaviour, against the CPU oracle:
+
+* in-place decode in the reference's two layouts (src/curve_mechanism_base.cpp:
+  222-260: plaintext where crypto_box_open_easy_afternm leaves it, and the
+  payload moved to the frame's start), for every frame-kernel variant and for
+  frames that take the chunked body path, with MAC and replay failures;
+* zmqg_*_batch_ex options: max_len (the body launches skipped, a broken bound
+  reported as ZMQG_ERR_BOUND), encode status, session maxima;
+* unknown sessions (ZMQG_ERR_SESSION instead of session 0);
+* the sharded-decode contract of SURVEY.md section 8e: two slices decoded one
+  after the other with peer_prefix equal one decode of the whole batch;
+* forged headers on 1 MiB and 16 MiB frames (mechanism_base.cpp:14-25,
+  curve_mechanism_base.cpp:85-96): zero-filled over the whole grid, no slower
+  than decoding the same frames when genuine;
+* a fresh ctx decoding at once on a non-blocking stream (no device syncs);
+* the multi-session replay tables (and the sort fallback above 8192
+  sessions) against the oracle's sequential rule.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import pack
+
+pytestmark = pytest.mark.gpu
+
+
+def t(torch, a, dtype=None):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a.copy()).to("cuda")
+
+
+def host(x, dtype):
+    return x.cpu().numpy().view(dtype)
+
+
+def _keys(rng, n):
+    return [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(n)]
+
+
+def _ctxs(C, keys, peer=2):
+    enc = C.CurveContext(0, len(keys))
+    dec = C.CurveContext(0, len(keys))
+    for s, k in enumerate(keys):
+        enc.session_set(s, k, O.CLIENT_PREFIX, O.SERVER_PREFIX)
+        dec.session_set(s, k, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, peer)
+    return enc, dec
+
+
+def _oracle_dec_sessions(keys):
+    return np.concatenate([O.make_sessions([k], dec_prefix=O.CLIENT_PREFIX) for k in keys])
+
+
+def _wire_batch(torch, C, rng, keys, sizes, sid, nonce, flags=None, gap=0):
+    """Encode frames with the oracle; returns (wire buffer, in_off, wire_len, payloads)."""
+    n = len(sizes)
+    flags = np.zeros(n, np.uint8) if flags is None else flags
+    pays = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+    inp, in_off = pack(pays, rng, 0)
+    wl = np.array([O.wire_size(int(f), 0, int(s)) for f, s in zip(flags, sizes)], np.uint32)
+    _, woff = pack([b"\0" * int(w) for w in wl], rng, gap, base_gap=40)
+    total = int(woff[-1]) + int(wl[-1]) + 64
+    sess = np.concatenate([O.make_sessions([k]) for k in keys])
+    wire = O.encode_batch(sess, sid, nonce, flags, in_off, np.array(sizes, np.uint32), inp, woff, total)
+    return wire, woff, wl, pays
+
+
+def _expected(keys, peer, sid, woff, wl, wire):
+    """Oracle decode (out of place): per-frame payload, flags, status."""
+    plen = wl.astype(np.int64) - 33
+    pout = np.zeros(len(wl), np.uint64)
+    pos = 0
+    for i, p in enumerate(plen):
+        pout[i] = pos
+        pos += max(int(p), 0)
+    out, fl, st = O.decode_batch(_oracle_dec_sessions(keys), peer, sid, woff, wl, wire, pout, pos + 1)
+    pays = [out[int(pout[i]):int(pout[i]) + max(int(plen[i]), 0)] for i in range(len(wl))]
+    return pays, fl, st
+
+
+# ------------------------------------------------------------------ in place
+@pytest.mark.parametrize("G", ["", "0", "2", "4"])
+@pytest.mark.parametrize("layout", [33, 0])
+def test_inplace_decode_layouts(torch_cuda, C, monkeypatch, G, layout):
+    """out == in with out_off = in_off + 33 or in_off: payloads, flags, status
+    and zero fills equal the oracle's out-of-place decode; bytes outside each
+    frame's payload region hold no plaintext."""
+    torch = torch_cuda
+    if G:
+        monkeypatch.setenv("ZMQG_FRAMES_G", G)
+    rng = np.random.default_rng(100 + layout + (int(G) if G else 9))
+    keys = _keys(rng, 3)
+    sizes = list(rng.choice(list(range(0, 140)) + [1024, 1025, 4000, 4575, 4576, 4600], 150))
+    sizes += [65536, 70001, 1 << 20, 200000, 4700]
+    n = len(sizes)
+    sid = rng.integers(0, 3, n).astype(np.uint32)
+    nonce = np.zeros(n, np.uint64)
+    nxt = [3, 3, 3]
+    for i in range(n):
+        nonce[i] = nxt[sid[i]]
+        nxt[sid[i]] += 1
+    flags = rng.choice([0, 1, 2, 3], n).astype(np.uint8)
+    wire, woff, wl, pays = _wire_batch(torch, C, rng, keys, sizes, sid, nonce, flags, gap=9)
+    # failures: MAC (small and big), replay
+    for i in (5, 77, n - 4, n - 3):
+        if wl[i] > 40:
+            wire[int(woff[i]) + int(wl[i]) - 1] ^= 0x10
+    j = next(k for k in range(60, n) if sid[k] == sid[50] and k > 50)
+    nonce_bytes = wire[int(woff[50]) + 8:int(woff[50]) + 16].copy()
+    wire[int(woff[j]) + 8:int(woff[j]) + 16] = nonce_bytes  # frame j replays frame 50 (its MAC now fails too)
+    peer = np.full(3, 2, np.uint64)
+    ref_pay, ref_fl, ref_st = _expected(keys, peer, sid, woff, wl, wire)
+    assert (ref_st != 0).sum() >= 4
+
+    _, dec = _ctxs(C, keys)
+    buf = t(torch, wire)
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    out_off = woff + np.uint64(layout)
+    dec.decode_batch(t(torch, sid), t(torch, woff), t(torch, wl), buf, t(torch, out_off), buf, fl, st)
+    torch.cuda.synchronize()
+    got = host(buf, np.uint8)
+    assert np.array_equal(host(st, np.int32), ref_st)
+    assert np.array_equal(host(fl, np.uint8), ref_fl)
+    for i in range(n):
+        a, L = int(woff[i]), int(wl[i])
+        if L < 33:
+            continue
+        p0 = a + layout
+        region = got[p0:p0 + L - 33]
+        if ref_st[i] == 0:
+            assert np.array_equal(region, ref_pay[i]), (i, L)
+        else:
+            assert not region.any(), (i, L, ref_st[i])
+            # no plaintext anywhere in the frame's wire region
+            if layout == 0:
+                tail = got[a + L - 33:a + L]
+                assert not tail.any() or np.array_equal(tail, wire[a + L - 33:a + L]), i
+    for s in range(3):
+        assert dec.get_peer_nonce(s) == int(peer[s])
+
+
+# ------------------------------------------------------------------ _ex options
+def test_ex_max_len_and_statuses(torch_cuda, C):
+    """max_len at the frame kernel's limit skips the body kernels (no body
+    launch is profiled); a frame above the bound fails with ERR_BOUND and its
+    region is left as it was; encode reports per-frame status; unknown
+    sessions fail with ERR_SESSION."""
+    torch = torch_cuda
+    rng = np.random.default_rng(7)
+    keys = _keys(rng, 2)
+    enc, dec = _ctxs(C, keys)
+    n = 64
+    sizes = np.full(n, 1024, np.uint32)
+    sizes[10] = 2048                   # above the bound
+    sid = (np.arange(n) % 2).astype(np.uint32)
+    sid_bad = sid.copy()
+    sid_bad[20] = 7                    # unknown session
+    nonce = (3 + np.arange(n) // 2).astype(np.uint64)
+    pays = [rng.integers(0, 256, int(s), dtype=np.uint8) for s in sizes]
+    inp, in_off = pack([p.tobytes() for p in pays])
+    W = sizes + 33
+    out_off = np.concatenate([[0], np.cumsum(W)[:-1]]).astype(np.uint64)
+    total = int(W.sum())
+    # encode with the bound 1024 and status
+    wire = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    est = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    enc.set_profiling(True)
+    enc.encode_batch(t(torch, sid_bad), t(torch, nonce), torch.zeros(n, dtype=torch.uint8, device="cuda"),
+                     t(torch, in_off), t(torch, sizes), t(torch, inp), t(torch, out_off), wire, max_len=1024,
+                     status_out=est)
+    torch.cuda.synchronize()
+    assert enc.get_profile(C.CurveContext.PROF_ENCODE_BODY)[1] == 0
+    enc.set_profiling(False)
+    e = host(est, np.int32)
+    assert e[10] == C.ERR_BOUND and e[20] == C.ERR_SESSION
+    assert (np.delete(e, [10, 20]) == 0).all()
+    w = host(wire, np.uint8)
+    sess = np.concatenate([O.make_sessions([k]) for k in keys])
+    ref = O.encode_batch(sess, sid, nonce, np.zeros(n, np.uint8), in_off, sizes, inp, out_off, total)
+    for i in range(n):
+        a, z = int(out_off[i]), int(out_off[i] + W[i])
+        if i in (10, 20):
+            assert (w[a:z] == 0xA5).all(), i
+        else:
+            assert np.array_equal(w[a:z], ref[a:z]), i
+    # decode the oracle's wire with the bound 1057 (frame 10 is 2081 bytes)
+    back = torch.full((int(sizes.sum()),), 0x5A, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    dec.set_profiling(True)
+    dec.decode_batch(t(torch, sid_bad), t(torch, out_off), t(torch, W), t(torch, ref), t(torch, in_off), back, fl, st,
+                     max_len=1057)
+    torch.cuda.synchronize()
+    assert dec.get_profile(C.CurveContext.PROF_DECODE_BODY)[1] == 0
+    dec.set_profiling(False)
+    s_ = host(st, np.int32)
+    b = host(back, np.uint8)
+    assert s_[10] == C.ERR_BOUND and s_[20] == C.ERR_SESSION
+    for i in range(n):
+        region = b[int(in_off[i]):int(in_off[i]) + int(sizes[i])]
+        if i == 10:
+            assert (region == 0x5A).all()
+        elif i == 20:
+            assert not region.any()
+        else:
+            assert s_[i] == 0 and np.array_equal(region, pays[i]), i
+    # the same batch without a bound: the body runs, frame 10 decodes
+    dec2 = _ctxs(C, keys)[1]
+    dec2.decode_batch(t(torch, sid), t(torch, out_off), t(torch, W), t(torch, ref), t(torch, in_off), back, fl, st)
+    torch.cuda.synchronize()
+    assert (host(st, np.int32) == 0).all()
+    assert np.array_equal(host(back, np.uint8)[int(in_off[10]):int(in_off[10]) + 2048], pays[10])
+
+
+@pytest.mark.parametrize("n_sessions", [1, 5])
+def test_session_max_out_and_header_pass(torch_cuda, C, n_sessions):
+    """decode's session_max_out and zmqg_session_max_batch both give each
+    session's largest header-valid nonce (forged headers excluded)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(20 + n_sessions)
+    keys = _keys(rng, n_sessions)
+    n = 3000
+    sizes = rng.integers(0, 300, n)
+    sid = rng.integers(0, n_sessions, n).astype(np.uint32)
+    nonce = rng.integers(3, 1 << 40, n).astype(np.uint64)
+    wire, woff, wl, _ = _wire_batch(torch, C, rng, keys, sizes, sid, nonce)
+    forged = rng.choice(n, 40, replace=False)
+    for i in forged:
+        wire[int(woff[i]) + 1] ^= 0xFF  # "\x07MESSAGE" broken: not header-valid
+    expect = np.zeros(n_sessions, np.uint64)
+    for i in range(n):
+        if i not in set(forged.tolist()):
+            expect[sid[i]] = max(expect[sid[i]], nonce[i])
+    _, dec = _ctxs(C, keys)
+    hp = torch.zeros(n_sessions, dtype=torch.int64, device="cuda")
+    dec.session_max_batch(t(torch, sid), t(torch, woff), t(torch, wl), t(torch, wire), hp)
+    smax = torch.zeros(n_sessions, dtype=torch.int64, device="cuda")
+    out = torch.zeros(int(wl.sum()) + 1, dtype=torch.uint8, device="cuda")
+    pout = np.concatenate([[0], np.cumsum(wl.astype(np.int64))[:-1]]).astype(np.uint64)
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    dec.decode_batch(t(torch, sid), t(torch, woff), t(torch, wl), t(torch, wire), t(torch, pout), out, fl, st,
+                     session_max_out=smax)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(hp, np.uint64), expect)
+    assert np.array_equal(host(smax, np.uint64), expect)
+    ref_pay, ref_fl, ref_st = _expected(keys, np.full(n_sessions, 2, np.uint64), sid, woff, wl, wire)
+    assert np.array_equal(host(st, np.int32), ref_st)
+
+
+def test_sharded_decode_peer_prefix(torch_cuda, C):
+    """Two ranks' slices of one batch, decoded one after the other on separate
+    contexts with peer nonces from shard.peer_prefix over the header pass,
+    equal one decode of the whole batch -- including replays whose earlier
+    nonce lies in the other slice."""
+    torch = torch_cuda
+    from libzmq_amd import shard
+    rng = np.random.default_rng(31)
+    S = 6
+    keys = _keys(rng, S)
+    n = 4000
+    sizes = rng.integers(0, 600, n)
+    sid = rng.integers(0, S, n).astype(np.uint32)
+    nonce = np.zeros(n, np.uint64)
+    nxt = [5] * S
+    for i in range(n):
+        nonce[i] = nxt[sid[i]]
+        nxt[sid[i]] += int(rng.integers(1, 3))
+    cut = 1700
+    for k in range(30):  # replays across the cut
+        i = int(rng.integers(cut, n))
+        cands = [j for j in range(max(0, cut - 200), cut) if sid[j] == sid[i]]
+        if cands:
+            nonce[i] = nonce[cands[int(rng.integers(0, len(cands)))]]
+    wire, woff, wl, _ = _wire_batch(torch, C, rng, keys, sizes, sid, nonce)
+    peer_before = np.full(S, 2, np.uint64)
+    pout = np.concatenate([[0], np.cumsum(wl.astype(np.int64))[:-1]]).astype(np.uint64)
+    size = int(wl.sum()) + 1
+
+    def decode(ctx, lo, hi):
+        out = torch.zeros(size, dtype=torch.uint8, device="cuda")
+        fl = torch.zeros(hi - lo, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(hi - lo, dtype=torch.int32, device="cuda")
+        ctx.decode_batch(t(torch, sid[lo:hi]), t(torch, woff[lo:hi]), t(torch, wl[lo:hi]), t(torch, wire),
+                         t(torch, pout[lo:hi]), out, fl, st)
+        torch.cuda.synchronize()
+        return host(out, np.uint8), host(fl, np.uint8), host(st, np.int32)
+
+    _, whole = _ctxs(C, keys)
+    w_out, w_fl, w_st = decode(whole, 0, n)
+    assert (w_st == C.ERR_INVALID_SEQUENCE).sum() >= 5
+    # rank maxima from the header pass, then the exclusive prefix per rank
+    maxima = []
+    for lo, hi in ((0, cut), (cut, n)):
+        _, c = _ctxs(C, keys)
+        m = torch.zeros(S, dtype=torch.int64, device="cuda")
+        c.session_max_batch(t(torch, sid[lo:hi]), t(torch, woff[lo:hi]), t(torch, wl[lo:hi]), t(torch, wire), m)
+        torch.cuda.synchronize()
+        maxima.append(host(m, np.uint64))
+    maxima = np.stack(maxima)
+    outs = []
+    final = np.zeros(S, np.uint64)
+    for r, (lo, hi) in enumerate(((0, cut), (cut, n))):
+        pre = shard.peer_prefix(maxima, peer_before, r)
+        _, c = _ctxs(C, keys)
+        for s in range(S):
+            c.set_peer_nonce(s, int(pre[s]))
+        outs.append(decode(c, lo, hi))
+        final = np.maximum(final, [c.get_peer_nonce(s) for s in range(S)])
+    st = np.concatenate([outs[0][2], outs[1][2]])
+    fl = np.concatenate([outs[0][1], outs[1][1]])
+    assert np.array_equal(st, w_st)
+    assert np.array_equal(fl, w_fl)
+    for i in range(n):
+        o = outs[0][0] if i < cut else outs[1][0]
+        a, z = int(pout[i]), int(pout[i]) + int(wl[i]) - 33
+        assert np.array_equal(o[a:z], w_out[a:z]), i
+    assert np.array_equal(final, [whole.get_peer_nonce(s) for s in range(S)])
+
+
+# ------------------------------------------------------------------ adversarial
+def test_forged_big_headers_zero_filled_fast(torch_cuda, C):
+    """1 MiB and 16 MiB frames with a broken "\\x07MESSAGE", short frames and
+    size <= data[0] among good frames: statuses as the oracle's, the forged
+    frames' payload regions zeroed, the neighbours intact -- and the call no
+    slower than decoding the same big frames genuine."""
+    torch = torch_cuda
+    rng = np.random.default_rng(55)
+    keys = _keys(rng, 1)
+    sizes = [1024] * 40 + [1 << 20, 16 << 20, 1 << 20] + [1024] * 40 + [16 << 20]
+    n = len(sizes)
+    sid = np.zeros(n, np.uint32)
+    nonce = np.arange(3, 3 + n, dtype=np.uint64)
+    wire, woff, wl, pays = _wire_batch(torch, C, rng, keys, sizes, sid, nonce)
+    good = wire.copy()
+    big = [i for i in range(n) if sizes[i] > 4096]
+    for i in big:
+        wire[int(woff[i]) + 3] ^= 0x40  # "\x07MESSAGE" broken
+    # short frames: size <= data[0] (7) and size < 33
+    wl_bad = wl.copy()
+    wl_bad[5] = 6
+    wl_bad[6] = 20
+    peer = np.full(1, 2, np.uint64)
+    ref_pay, ref_fl, ref_st = _expected(keys, peer, sid, woff, wl_bad, wire)
+    assert all(ref_st[i] == C.ERR_UNEXPECTED_COMMAND for i in big)
+    assert ref_st[5] == C.ERR_MALFORMED_UNSPECIFIED and ref_st[6] == C.ERR_MALFORMED_MESSAGE
+
+    pout = np.concatenate([[0], np.cumsum(np.maximum(wl.astype(np.int64) - 33, 0))[:-1]]).astype(np.uint64)
+    size = int(pout[-1]) + int(wl[-1])
+    out = torch.full((size,), 0x5A, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    d_sid, d_woff, d_pout = t(torch, sid), t(torch, woff), t(torch, pout)
+    d_bad, d_good = t(torch, wire), t(torch, good)
+    d_wlb, d_wl = t(torch, wl_bad), t(torch, wl)
+
+    def run(ctx, w, L):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        ctx.decode_batch(d_sid, d_woff, L, w, d_pout, out, fl, st)
+        ev1.record()
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1)
+
+    _, dec = _ctxs(C, keys)
+    run(dec, d_bad, d_wlb)
+    got = host(out, np.uint8)
+    assert np.array_equal(host(st, np.int32), ref_st)
+    for i in range(n):
+        p = int(wl_bad[i]) - 33
+        if p < 0:
+            continue
+        region = got[int(pout[i]):int(pout[i]) + p]
+        if ref_st[i]:
+            assert not region.any(), i
+        else:
+            assert np.array_equal(region, ref_pay[i]), i
+    # timing: forged vs genuine big frames (fresh contexts, nonces from 2)
+    t_bad = min(run(_ctxs(C, keys)[1], d_bad, d_wlb) for _ in range(3))
+    t_good = min(run(_ctxs(C, keys)[1], d_good, d_wl) for _ in range(3))
+    assert t_bad <= 1.25 * t_good + 0.05, (t_bad, t_good)
+
+
+# ------------------------------------------------------------------ streams
+def test_fresh_ctx_decodes_at_once_on_nonblocking_stream(torch_cuda, C):
+    """ctx creation, session install and an immediate decode on a
+    non-blocking stream: the ctx's tables are ready in stream order (no
+    device-wide synchronisation in create or workspace growth)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    keys = _keys(rng, 1)
+    n = 5000
+    sizes = rng.integers(0, 2000, n)
+    sid = np.zeros(n, np.uint32)
+    nonce = np.arange(3, 3 + n, dtype=np.uint64)
+    wire, woff, wl, pays = _wire_batch(torch, C, rng, keys, sizes, sid, nonce)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        d_sid, d_woff, d_wl, d_wire = t(torch, sid), t(torch, woff), t(torch, wl), t(torch, wire)
+        pout = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        d_pout = t(torch, pout)
+        out = torch.zeros(int(sizes.sum()) + 1, dtype=torch.uint8, device="cuda")
+        fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    stream.synchronize()
+    dec = C.CurveContext(0, 1)
+    dec.session_set(0, keys[0], O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    dec.decode_batch(d_sid, d_woff, d_wl, d_wire, d_pout, out, fl, st, stream=stream)
+    stream.synchronize()
+    assert (host(st, np.int32) == 0).all()
+    got = host(out, np.uint8)
+    for i in range(0, n, 97):
+        assert np.array_equal(got[int(pout[i]):int(pout[i]) + int(sizes[i])], np.frombuffer(pays[i], np.uint8))
+    assert dec.get_peer_nonce(0) == n + 2
+
+
+# ------------------------------------------------------------------ replay tables
+@pytest.mark.parametrize("n_sessions,n", [(1000, 40000), (37, 9000), (9000, 3000)])
+def test_multi_session_replay_vs_oracle(torch_cuda, C, n_sessions, n):
+    """Random session order (sessions repeating inside a wave), random
+    nonce gaps and replays, forged headers: statuses, flags, payloads and
+    final peer nonces equal the oracle's sequential decode (9000 sessions: the
+    sort fallback)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(n_sessions)
+    keys = _keys(rng, n_sessions)
+    sizes = rng.integers(0, 200, n)
+    sid = rng.integers(0, n_sessions, n).astype(np.uint32)
+    sid[100:164] = sid[100]  # one session filling a whole wave
+    nonce = rng.integers(3, 60, n).astype(np.uint64) + np.arange(n, dtype=np.uint64) // 3
+    flags = rng.choice([0, 1, 3], n).astype(np.uint8)
+    wire, woff, wl, _ = _wire_batch(torch, C, rng, keys, sizes, sid, nonce, flags)
+    for i in rng.choice(n, 25, replace=False):
+        wire[int(woff[i]) + 2] ^= 1
+    peer = np.full(n_sessions, 2, np.uint64)
+    ref_pay, ref_fl, ref_st = _expected(keys, peer, sid, woff, wl, wire)
+    assert (ref_st == C.ERR_INVALID_SEQUENCE).sum() > n // 50
+    _, dec = _ctxs(C, keys)
+    pout = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    out = torch.full((int(sizes.sum()) + 1,), 0x33, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    smax = torch.zeros(n_sessions, dtype=torch.int64, device="cuda")
+    dec.decode_batch(t(torch, sid), t(torch, woff), t(torch, wl), t(torch, wire), t(torch, pout), out, fl, st,
+                     session_max_out=smax)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(st, np.int32), ref_st)
+    assert np.array_equal(host(fl, np.uint8), ref_fl)
+    got = host(out, np.uint8)
+    for i in range(n):
+        a = int(pout[i])
+        if ref_st[i] == 0:
+            assert np.array_equal(got[a:a + int(sizes[i])], ref_pay[i]), i
+        else:
+            assert not got[a:a + int(sizes[i])].any(), i
+    final = [dec.get_peer_nonce(s) for s in range(n_sessions)]
+    assert np.array_equal(np.array(final, np.uint64), peer)
+    hv = np.zeros(n_sessions, np.uint64)
+    ok = np.isin(ref_st, [0, C.ERR_CRYPTOGRAPHIC, C.ERR_INVALID_SEQUENCE])
+    np.maximum.at(hv, sid[ok].astype(np.int64), nonce[ok])
+    assert np.array_equal(host(smax, np.uint64), hv)

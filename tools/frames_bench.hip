@@ -128,7 +128,7 @@ int main(int argc, char **argv)
         CHECK(hipMemset(d_wire, 0, wb));
         double te = timeit([&] {
             hipLaunchKernelGGL(kenc, dim3(blocks), dim3(256), 0, 0, n, d_sid, d_nonce, d_flags, d_ioff, d_len, d_pay,
-                               d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr, rpo, NoBigFrames{}, d_zs);
+                               d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr, rpo, NoBigFrames{}, d_zs, FrameCtl{});
         });
         CHECK(hipMemcpy(h_new.data(), d_wire, wb, hipMemcpyDeviceToHost));
         size_t bad = 0, first = (size_t) -1;
@@ -139,7 +139,7 @@ int main(int argc, char **argv)
         double td = timeit([&] {
             hipLaunchKernelGGL(kdec, dim3(blocks), dim3(256), 0, 0, n, d_sid, (const uint64_t *) nullptr,
                                (const uint8_t *) nullptr, d_ooff, d_wl, d_ref, d_ioff, d_back, d_ses, 1u, 0xffffffffu,
-                               d_fl, d_st, rpo, NoBigFrames{}, d_zs);
+                               d_fl, d_st, rpo, NoBigFrames{}, d_zs, FrameCtl{});
         });
         CHECK(hipMemcpy(h_back.data(), d_back, pay.size(), hipMemcpyDeviceToHost));
         std::vector<int32_t> st(n);
@@ -187,7 +187,7 @@ int main(int argc, char **argv)
         double te = timeit([&] {
             hipLaunchKernelGGL((k_frames<false, 2, NoBigFrames>), dim3(blocks), dim3(256), 0, 0, n, d_sid, d_nonce,
                                d_flags, d_ioff, d_len, d_pay, d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr, nullptr,
-                               rpo, NoBigFrames{}, d_zs);
+                               rpo, NoBigFrames{}, d_zs, FrameCtl{});
         });
         printf("G=2 encode only: %.1f us\n", te);
         return 0;
@@ -214,7 +214,7 @@ int main(int argc, char **argv)
             r.lb_inc = lbi;
             hipLaunchKernelGGL((k_frames<true, 2, NoBigFrames>), dim3(blocks), dim3(256), 0, 0, n, d_sid,
                                (const uint64_t *) nullptr, (const uint8_t *) nullptr, d_ooff, d_wl, d_ref, d_ioff,
-                               d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, r, NoBigFrames{}, d_zs);
+                               d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, r, NoBigFrames{}, d_zs, FrameCtl{});
         });
         printf("dbg=%u: %.1f us\n", dbg, td);
         }

@@ -70,11 +70,11 @@ int main()
             if (!dec)
                 hipLaunchKernelGGL((k_frames_seq<false, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid, d_nonce,
                                    d_flags, d_ioff, d_len, d_pay, d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr,
-                                   nullptr, rp, NoBigFrames{}, d_zs);
+                                   nullptr, rp, NoBigFrames{}, d_zs, FrameCtl{});
             else
                 hipLaunchKernelGGL((k_frames_seq<true, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid,
                                    (const uint64_t *) nullptr, (const uint8_t *) nullptr, d_ooff, d_wl, d_wire, d_ioff,
-                                   d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, NoBigFrames{}, d_zs);
+                                   d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, NoBigFrames{}, d_zs, FrameCtl{});
             CHECK(hipDeviceSynchronize());
         }
         std::vector<unsigned long long> c(64 * nwaves);
