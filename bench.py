@@ -85,6 +85,7 @@ def main():
 
     enc = C.CurveContext(local, 1)
     enc.session_set(0, precom, C.CLIENT_PREFIX, C.SERVER_PREFIX)
+    enc.set_nonce(0, 3)  # the handshake used nonces 1 and 2 (curve_client_t: HELLO, INITIATE)
     dec = C.CurveContext(local, 1)
     dec.session_set(0, precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
 
@@ -97,17 +98,20 @@ def main():
     lens = i32(np.full(n, P, np.uint32))
     out_off = i64(np.arange(n, dtype=np.uint64) * W)
     wlen = i32(np.full(n, W, np.uint32))
-    nonce = i64(np.arange(3, 3 + n, dtype=np.uint64))
     wire = torch.zeros(n * W, dtype=torch.uint8, device=dev)
     back = torch.zeros(n * P, dtype=torch.uint8, device=dev)
     fl_out = torch.zeros(n, dtype=torch.uint8, device=dev)
     st_out = torch.zeros(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    # One step = the I/O thread's batch call pair: encode with the nonces the
+    # session's send counter assigns on the device (ZMQG_OPT_NONCE_AUTO: the
+    # reference's get_and_inc_nonce per message), then decode of that wire.
+    # max_len = P: the batcher knows its frames' lengths, and a bound within the
+    # frame kernel's range skips the large-frame launches (include/zmqg_curve.h).
     def step(st):
-        enc.encode_batch(sid, nonce, flags, in_off, lens, payload, out_off, wire, st)
-        dec.decode_batch(sid, out_off, wlen, wire, in_off, back, fl_out, st_out, st)
-        nonce.add_(n)
+        enc.encode_batch(sid, None, flags, in_off, lens, payload, out_off, wire, st, max_len=P, nonce_auto=True)
+        dec.decode_batch(sid, out_off, wlen, wire, in_off, back, fl_out, st_out, st, max_len=W)
 
     for _ in range(args.warmup):
         step(stream)
@@ -331,10 +335,26 @@ def host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_o
     return out
 
 
+def host_cores():
+    """(threads to use, CPUs in the affinity mask, cgroup v2 CPU quota or None)."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(affinity, quota) if quota else affinity), affinity, quota
+
+
 def cpu_baseline(payload, precom, n, P, W, flags_np, seconds):
     from oracle import oracle as O
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    # one thread per host core this process may use (BASELINE.md: every
+    # core): the CPUs in its affinity mask, capped by its cgroup CPU quota
+    # (a GPU box's share of a larger host: the mask shows the whole host)
+    threads, affinity, quota = host_cores()
     # sessions partitioned across threads (one I/O thread owns a connection)
     S = threads
     sess = O.make_sessions([precom] * S)
@@ -356,7 +376,8 @@ def cpu_baseline(payload, precom, n, P, W, flags_np, seconds):
         passes += 1
         oks += ok
     assert oks == passes * n
-    return {"value": passes * n * P / 2**30 / total_s, "unit": "GiB/s", "cores": threads, "kind": "port",
+    return {"value": passes * n * P / 2**30 / total_s, "unit": "GiB/s", "cores": threads,
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(), "kind": "port",
             "msgs_per_s": passes * n / total_s,
             "sample": f"{passes} passes x {n} x {P} B encode+decode round trips ({total_s:.2f} s wall, "
                       f"{threads} threads, {S} sessions); crypto: {kind}; framing: oracle/curve_oracle.c "

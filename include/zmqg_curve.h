@@ -23,11 +23,15 @@
  *     src/curve_mechanism_base.hpp:36                zmqg_session_set (precom)
  *   curve_encoding_t::set_peer_nonce
  *     src/curve_mechanism_base.hpp:42                zmqg_session_set_peer_nonce
+ *   curve_encoding_t::get_and_inc_nonce (_cn_nonce)
+ *     src/curve_mechanism_base.hpp:41                ZMQG_OPT_NONCE_AUTO,
+ *                                                    zmqg_session_*_nonce
  *
  * One call processes a batch of independent MESSAGE frames.  Each frame
  * belongs to a session (one CURVE connection = one curve_encoding_t).  The
- * caller assigns encode nonces (the reference's get_and_inc_nonce,
- * src/curve_mechanism_base.hpp:41).  Decode applies the reference's replay
+ * caller assigns encode nonces, or lets the device take them from each
+ * session's send counter (ZMQG_OPT_NONCE_AUTO; the reference's
+ * get_and_inc_nonce, src/curve_mechanism_base.hpp:41).  Decode applies the reference's replay
  * rule exactly as if curve_encoding_t::decode had been called on the batch's
  * frames one by one in batch order, and updates each session's peer nonce.
  *
@@ -55,7 +59,7 @@
 extern "C" {
 #endif
 
-#define ZMQG_CURVE_ABI_VERSION 2
+#define ZMQG_CURVE_ABI_VERSION 3
 
 /* Per-frame status codes, identical to include/zmq.h:424-437. */
 #define ZMQG_STATUS_OK 0
@@ -107,6 +111,14 @@ int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], cons
 int zmqg_session_set_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t peer_nonce);
 int zmqg_session_get_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *peer_nonce_out);
 
+/* The session's send nonce (_cn_nonce, src/curve_mechanism_base.hpp:41-50):
+ * the next nonce zmqg_encode_batch_ex assigns under ZMQG_OPT_NONCE_AUTO.
+ * zmqg_session_set starts it at 1, as the reference's constructor does
+ * (src/curve_mechanism_base.cpp:59); set it after the handshake has used its
+ * nonces.  Synchronous, ordered like the peer-nonce accessors. */
+int zmqg_session_set_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce);
+int zmqg_session_get_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *nonce_out);
+
 /* Bytes of the encoded frame for a payload of `payload_len` bytes and msg_t
  * flags `msg_flags`: "\x07MESSAGE"(8) + nonce(8) + tag(16) + mlen, where
  * mlen = 1 + [1 | 7 | 10 for SUBSCRIBE/CANCEL] + payload_len
@@ -157,6 +169,14 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
 /* Options of the _ex batch calls (every field optional: a zeroed struct, or
  * opts = NULL, gives the plain calls' behaviour).
  *   size             sizeof(zmqg_batch_opts) (ABI check)
+ *   flags            ZMQG_OPT_NONCE_AUTO (encode): ignore `nonce` (it may be
+ *                    NULL) and take each frame's nonce from its session's
+ *                    send counter on the device, in batch order, as
+ *                    curve_encoding_t::get_and_inc_nonce does per message
+ *                    (src/curve_mechanism_base.hpp:41, called at
+ *                    src/curve_mechanism_base.cpp:116); the counters advance
+ *                    by each session's frame count.  Several sessions: at
+ *                    most 8192 (-EINVAL above).
  *   max_len          0, or a bound on every len[i] (encode) / wire_len[i]
  *                    (decode).  A bound under which every frame fits the frame
  *                    kernel (stream <= 4.5 KiB: decode wire_len <= 4608, encode
@@ -170,9 +190,10 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  *                    batch's frames (0 where it has none) -- the value a rank
  *                    contributes to shard.peer_prefix when a session's frames
  *                    span GPUs. */
+#define ZMQG_OPT_NONCE_AUTO 1u
 typedef struct zmqg_batch_opts {
     uint32_t size;
-    uint32_t reserved;
+    uint32_t flags;
     uint64_t max_len;
     int32_t *status_out;
     uint64_t *session_max_out;

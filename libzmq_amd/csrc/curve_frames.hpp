@@ -38,7 +38,7 @@
 #pragma once
 
 #ifndef ZMQG_FRAMES_ABLATE
-#define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: 1 no Poly1305, 2 no stores, 4 no input shift
+#define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: k_frames: 1 no Poly1305, 2 no stores, 4 no input shift; k_frames_seq: 8 no stores, 16 no loads, 32 no Salsa20, 64 no Poly1305
 #endif
 
 #ifndef ZMQG_FR_BS
@@ -335,7 +335,24 @@ struct FrameCtl {
     uint64_t max_len;    // 0, or the caller's bound on len / wire_len
     uint32_t no_body;    // 1: no body kernel follows (every frame within max_len fits this kernel)
     uint32_t pad;
+    unsigned long long *nonce_ctr; // encode, one session, ZMQG_OPT_NONCE_AUTO: the session's send
+                                   // counter; frame i takes *nonce_ctr + i, the last workgroup adds n
 };
+
+// Encode nonce of frame i: the caller's, or (ZMQG_OPT_NONCE_AUTO, one
+// session) the send counter read at kernel start plus i, as n calls of
+// curve_encoding_t::get_and_inc_nonce (src/curve_mechanism_base.hpp:41) would
+// assign them.
+__device__ __forceinline__ uint64_t frame_nonce(const uint64_t *nonce, const FrameCtl &ctl, uint64_t nbase,
+                                                uint32_t i)
+{
+    return ctl.nonce_ctr ? nbase + i : nonce[i];
+}
+
+__device__ __forceinline__ uint64_t nonce_base(const FrameCtl &ctl)
+{
+    return ctl.nonce_ctr ? __hip_atomic_load(ctl.nonce_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+}
 
 // Frames whose region a failing lane zero-fills itself; longer ones go to
 // the post list (k_post spreads them over the whole grid).
@@ -465,6 +482,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     const uint32_t epoch = sh_epoch;
     if (lb && !rp.ordered && !(rp.dbg & 2))
         wg = sh_ticket;
+    const uint64_t nbase = DEC ? 0ull : nonce_base(ctl);
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0; // the next call's list (the previous body has finished with it)
@@ -491,7 +509,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     int32_t status = 0;
     uint32_t hw[3] = {0, 0, 0};
     if (!DEC) {
-        const uint64_t nc = nonce[ii];
+        const uint64_t nc = frame_nonce(nonce, ctl, nbase, ii);
         n0 = bswap32((uint32_t) (nc >> 32));
         n1 = bswap32((uint32_t) nc);
         hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
@@ -871,6 +889,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
             __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!DEC && ctl.nonce_ctr) // every workgroup has read the counter
+                __hip_atomic_store(ctl.nonce_ctr, nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     if (!DEC && valid && q == 0 && ctl.enc_status)
@@ -993,6 +1013,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     const uint32_t epoch = sh_epoch;
     if (lb && !rp.ordered)
         wg = sh_ticket;
+    const uint64_t nbase = DEC ? 0ull : nonce_base(ctl);
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
@@ -1018,7 +1039,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     uint32_t hw[3] = {0, 0, 0};
     uint32_t x0[16], d0 = 0; // window 0's stream words (decode: the wire; encode: payload bytes 0..), word 16
     if (!DEC) {
-        const uint64_t nc = nonce[ii];
+        const uint64_t nc = frame_nonce(nonce, ctl, nbase, ii);
         n0 = bswap32((uint32_t) (nc >> 32));
         n1 = bswap32((uint32_t) nc);
         hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
@@ -1208,7 +1229,13 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         SEQ_STAMP(3u + t);
         const bool act = t < nw;
         uint32_t ks[16];
-        salsa20_block(ks, key, n0, n1, t, 0);
+        if (ZMQG_FRAMES_ABLATE & 32) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                ks[k] = key[k & 7] ^ (t * 0x9e3779b9u + k);
+        } else {
+            salsa20_block(ks, key, n0, n1, t, 0);
+        }
         // The previous window's MAC (its ciphertext is in cp).  The
         // four-block form runs for every lane, unconditionally, so that it
         // shares a basic block with the keystream and the scheduler
@@ -1218,7 +1245,10 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         const bool full = pv && cp_j0 == 0u && cp_len == 64u;
         {
             Poly32 hf = h;
-            poly32_window_full(hf, pk, cp);
+            if (ZMQG_FRAMES_ABLATE & 64)
+                hf.h0 ^= cp[0] ^ cp[5] ^ cp[11];
+            else
+                poly32_window_full(hf, pk, cp);
             h.h0 = full ? hf.h0 : h.h0;
             h.h1 = full ? hf.h1 : h.h1;
             h.h2 = full ? hf.h2 : h.h2;
@@ -1232,7 +1262,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         for (int k = 0; k < 16; ++k)
             asm volatile("" : "+v"(ks[k]));
         asm volatile("" : "+v"(h.h0), "+v"(h.h1), "+v"(h.h2), "+v"(h.h3), "+v"(h.h4));
-        if (__builtin_amdgcn_ballot_w64(pv && !full) != 0) {
+        if (!(ZMQG_FRAMES_ABLATE & 64) && __builtin_amdgcn_ballot_w64(pv && !full) != 0) {
             if (pv && !full)
                 poly32_window(h, pk, cp, cp_j0, cp_len);
         }
@@ -1262,6 +1292,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             w16 = dd[15];
         }
         d0 = w16;
+        if (t < 8u)
+            SEQ_STAMP(44u + t);
         const bool tail = act && S < 64u * t + 64u;
         if (DEC && __builtin_amdgcn_ballot_w64(tail) != 0) {
             if (tail)
@@ -1283,11 +1315,25 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         // window t+1's loads and window t's stores, issued together after
         // the input has been consumed: the wait for the loads comes a whole
         // keystream later
-        if (t + 1u < nw)
+        if (ZMQG_FRAMES_ABLATE & 16) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                dn[k] = y[k] + k;
+            fastn = true;
+        } else if (t + 1u < nw) {
             fastn = frame_prefetch(A4, lim, wave_end, t + 1u, dn);
-        if (act)
+        }
+        if (t < 8u)
+            SEQ_STAMP(52u + t);
+        if (ZMQG_FRAMES_ABLATE & 8) {
+            if (act && y[3] == 0x12345678u && y[7] == ycarry)
+                *(GU32 *) (uintptr_t) B = y[0];
+        } else if (act) {
             frame_store(B, t, S, y, ycarry, t + 1u == nw);
+        }
         ycarry = y[15];
+        if (t < 8u)
+            SEQ_STAMP(36u + t);
     };
 #pragma unroll 1
     for (uint32_t t = 1; t < steps; t += 2) {
@@ -1328,6 +1374,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!DEC && ctl.nonce_ctr) // every workgroup has read the counter
+                __hip_atomic_store(ctl.nonce_ctr, nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     SEQ_STAMP(61u);

@@ -145,7 +145,8 @@ struct Workspace {
     unsigned long long *lb_inc = nullptr;   // [cap]
     void *temp = nullptr;
     size_t temp_bytes = 0;
-    unsigned long long *rt = nullptr; // replay tables: [tiles][S] then [row blocks][S]
+    unsigned long long *rt = nullptr; // replay tables: [tiles][S] then [row blocks][S] (also the nonce tables)
+    uint64_t *nonce = nullptr;        // [cap] ZMQG_OPT_NONCE_AUTO over several sessions: each frame's nonce
     size_t rt_cap = 0;
     bool use_last = false; // the last replay ran the sort fallback (k_fixup writes the peer nonces)
 };
@@ -183,6 +184,7 @@ struct zmqg_ctx {
     int sort_bits = 0;
     DevSession *sessions = nullptr;
     unsigned long long *peer = nullptr; // [max_sessions]
+    unsigned long long *send = nullptr; // [max_sessions] send nonces (_cn_nonce) for ZMQG_OPT_NONCE_AUTO
     Workspace ws;
     ZmtpWs zw;
     // host staging for the *_host entry points
@@ -300,7 +302,8 @@ __device__ void head_powers(const fe &r, uint32_t nch, uint32_t blast, FramePow 
 // =====================================================================
 // session setup
 // =====================================================================
-__global__ void k_session_setup(DevSession *tab, unsigned long long *peer, uint32_t sid, const uint32_t *in)
+__global__ void k_session_setup(DevSession *tab, unsigned long long *peer, unsigned long long *send, uint32_t sid,
+                                const uint32_t *in)
 {
     // in: precom[8] enc_prefix[4] dec_prefix[4] downgrade peer_lo peer_hi
     if (threadIdx.x != 0)
@@ -316,12 +319,20 @@ __global__ void k_session_setup(DevSession *tab, unsigned long long *peer, uint3
         s.pad[i] = 0;
     tab[sid] = s;
     peer[sid] = ((unsigned long long) in[18] << 32) | in[17];
+    send[sid] = 1; // _cn_nonce (1), src/curve_mechanism_base.cpp:59
 }
 
-__global__ void k_set_peer(unsigned long long *peer, uint32_t sid, unsigned long long v)
+__global__ void k_fill_u64(unsigned long long *p, uint32_t n, unsigned long long v)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        p[i] = v;
+}
+
+__global__ void k_set_peer(unsigned long long *arr, uint32_t sid, unsigned long long v)
 {
     if (threadIdx.x == 0)
-        peer[sid] = v;
+        arr[sid] = v;
 }
 
 // =====================================================================
@@ -367,6 +378,7 @@ struct EncodeHead {
     const DevSession *sessions;
     uint32_t max_sessions;
     BigRecords R;
+    const unsigned long long *nonce_ctr; // ZMQG_OPT_NONCE_AUTO, one session (FrameCtl::nonce_ctr)
     __device__ void operator()(uint32_t i, unsigned long long *list_ctr) const;
 };
 
@@ -391,7 +403,8 @@ __device__ void EncodeHead::operator()(uint32_t i, unsigned long long *list_ctr)
 #pragma unroll
     for (int t = 0; t < 8; ++t)
         H.key[t] = ses.enc_key[t];
-    const uint64_t nc = nonce[i];
+    const uint64_t nc =
+        nonce_ctr ? __hip_atomic_load(nonce_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + i : nonce[i];
     const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
 
     uint32_t ks[16];
@@ -845,6 +858,112 @@ __global__ __launch_bounds__(64) void k_replay_frames(uint32_t n, uint32_t T, ui
     }
 }
 
+// ---------------------------------------------------------------- send nonces
+// ZMQG_OPT_NONCE_AUTO over several sessions: frame i of session s takes
+// send[s] + (frames of s before i in the batch), and send[s] advances by the
+// session's frame count -- get_and_inc_nonce per message in batch order
+// (src/curve_mechanism_base.hpp:41).  Same tile tables as the replay prefix,
+// with counts and sums in place of maxima:
+//   k_nonce_tiles    per tile, per-session frame counts -> tab[t][s]
+//   k_nonce_colblk   per session and block of kReplayRB rows: the block sum
+//   k_nonce_colscan  tab[t][s] := send[s] + frames of s in tiles < t; the last
+//                    block advances send[s]
+//   k_nonce_frames   one wave per tile: nonce = tab[t][sid] + earlier frames
+//                    of the session in the tile (lanes grouped by session
+//                    with ballots, 64 frames at a time)
+__global__ __launch_bounds__(256) void k_nonce_tiles(uint32_t n, uint32_t T, uint32_t S,
+                                                    const uint32_t *__restrict__ sid,
+                                                    unsigned long long *__restrict__ tab)
+{
+    extern __shared__ unsigned long long sh_tab[];
+    uint32_t *const cnt = (uint32_t *) sh_tab;
+    for (uint32_t k = threadIdx.x; k < S; k += 256)
+        cnt[k] = 0;
+    __syncthreads();
+    const uint64_t b = (uint64_t) blockIdx.x * T, e = b + T < n ? b + T : n;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 256) {
+        const uint32_t s = sid[i];
+        if (s < S)
+            atomicAdd(cnt + s, 1u);
+    }
+    __syncthreads();
+    unsigned long long *row = tab + (size_t) blockIdx.x * S;
+    for (uint32_t k = threadIdx.x; k < S; k += 256)
+        row[k] = cnt[k];
+}
+
+__global__ __launch_bounds__(256) void k_nonce_colblk(uint32_t tiles, uint32_t S,
+                                                     const unsigned long long *__restrict__ tab,
+                                                     unsigned long long *__restrict__ blk)
+{
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x, rb = blockIdx.y;
+    if (s >= S)
+        return;
+    const uint32_t r0 = rb * kReplayRB, r1 = r0 + kReplayRB < tiles ? r0 + kReplayRB : tiles;
+    unsigned long long m = 0;
+    for (uint32_t r = r0; r < r1; ++r)
+        m += tab[(size_t) r * S + s];
+    blk[(size_t) rb * S + s] = m;
+}
+
+__global__ __launch_bounds__(256) void k_nonce_colscan(uint32_t tiles, uint32_t S, unsigned long long *__restrict__ tab,
+                                                      const unsigned long long *__restrict__ blk,
+                                                      unsigned long long *__restrict__ send)
+{
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x, rb = blockIdx.y;
+    if (s >= S)
+        return;
+    unsigned long long m = send[s];
+    for (uint32_t k = 0; k < rb; ++k)
+        m += blk[(size_t) k * S + s];
+    const uint32_t r0 = rb * kReplayRB, r1 = r0 + kReplayRB < tiles ? r0 + kReplayRB : tiles;
+    for (uint32_t r = r0; r < r1; ++r) {
+        unsigned long long *p = tab + (size_t) r * S + s;
+        const unsigned long long x = *p;
+        *p = m;
+        m += x;
+    }
+    if (r1 == tiles) // every block has read send[s] above (k_nonce_frames runs after this kernel)
+        send[s] = m;
+}
+
+__global__ __launch_bounds__(64) void k_nonce_frames(uint32_t n, uint32_t T, uint32_t S,
+                                                    const uint32_t *__restrict__ sid,
+                                                    const unsigned long long *__restrict__ tab,
+                                                    uint64_t *__restrict__ nonce)
+{
+    extern __shared__ unsigned long long sh_tab[]; // [S] the next nonce of each session
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long *row = tab + (size_t) blockIdx.x * S;
+    for (uint32_t k = lane; k < S; k += 64)
+        sh_tab[k] = row[k];
+    __syncthreads();
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const uint64_t b = (uint64_t) blockIdx.x * T, e = b + T < n ? b + T : n;
+    for (uint64_t i0 = b; i0 < e; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const bool in = i < e && sid[i] < S;
+        const uint32_t s = in ? sid[i] : 0u;
+        unsigned long long left = __builtin_amdgcn_ballot_w64(in);
+        uint64_t v = 0;
+        while (left) { // one session per round: its lanes, in lane (= batch) order
+            const uint32_t lead = (uint32_t) __builtin_ctzll(left);
+            const uint32_t sl = (uint32_t) __builtin_amdgcn_readlane((int) s, (int) lead);
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(in && s == sl);
+            const unsigned long long base = sh_tab[sl];
+            if (in && s == sl)
+                v = base + (unsigned long long) __builtin_popcountll(m & below);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == lead)
+                sh_tab[sl] = base + (unsigned long long) __builtin_popcountll(m);
+            __builtin_amdgcn_wave_barrier();
+            left &= ~m;
+        }
+        if (i < e)
+            nonce[i] = v;
+    }
+}
+
 // ---------------------------------------------------------------- body
 // One lane per chunk (2 Salsa20 blocks = 128 stream bytes = 8 Poly1305
 // blocks); a tile is 64 consecutive chunks, one wave's worth, so a tile's
@@ -1207,6 +1326,8 @@ __global__ __launch_bounds__(256) void k_post(ZState *__restrict__ zs, const Pos
                                               uint8_t *__restrict__ seam)
 {
     const uint32_t np = zs->post_n; // appended by the kernels before this one (stream order)
+    if (np == 0)
+        return; // nothing listed: no fence, no counter (post_done stays 0)
     const uint32_t G = gridDim.x;
     for (uint32_t e = 0; e < np; ++e) {
         const PostOp o = post[e];
@@ -1557,7 +1678,8 @@ int ensure_workspace(zmqg_ctx *ctx, uint64_t n, hipStream_t st)
             (rc = grow(ctx, w.perm, cap, st)) || (rc = grow(ctx, w.keys_s, cap, st)) || (rc = grow(ctx, w.last, cap, st)) ||
             (rc = grow(ctx, w.list_frame, cap, st)) || (rc = grow(ctx, w.post, cap, st)) ||
             (rc = grow(ctx, w.psnap, cap, st)) || (rc = grow(ctx, w.blockmax, cap, st)) ||
-            (rc = grow(ctx, w.lb_flag, cap, st)) || (rc = grow(ctx, w.lb_agg, cap, st)) || (rc = grow(ctx, w.lb_inc, cap, st)))
+            (rc = grow(ctx, w.lb_flag, cap, st)) || (rc = grow(ctx, w.lb_agg, cap, st)) || (rc = grow(ctx, w.lb_inc, cap, st)) ||
+            (rc = grow(ctx, w.nonce, cap, st)))
             return rc;
         ZCHECK(ctx, hipMemsetAsync(w.lb_flag, 0, cap * sizeof(unsigned long long), st));
         if (!w.zs) {
@@ -1698,6 +1820,40 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
 #undef ZMQG_LAUNCH_FRAMES
 }
 
+// ZMQG_OPT_NONCE_AUTO over several sessions: each frame's nonce into w.nonce
+// (k_nonce_*), advancing the sessions' send counters, on `st` before the
+// frame kernel.
+int nonce_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st)
+{
+    Workspace &w = ctx->ws;
+    const uint32_t S = ctx->max_sessions;
+    uint32_t T = 4096;
+    while ((nn + T - 1) / T > kReplayMaxTiles)
+        T *= 2;
+    const uint32_t tiles = (nn + T - 1) / T, rbs = (tiles + kReplayRB - 1) / kReplayRB;
+    const size_t need = ((size_t) tiles + rbs) * S;
+    if (need > w.rt_cap) {
+        if (w.rt)
+            ZCHECK(ctx, hipFreeAsync(w.rt, st));
+        w.rt = nullptr;
+        ZCHECK(ctx, hipMallocAsync((void **) &w.rt, need * sizeof(unsigned long long), st));
+        w.rt_cap = need;
+    }
+    unsigned long long *tab = w.rt, *blk = w.rt + (size_t) tiles * S;
+    hipLaunchKernelGGL(k_nonce_tiles, dim3(tiles), dim3(256), S * sizeof(uint32_t), st, nn, T, S, sid, tab);
+    ZCHECK(ctx, hipGetLastError());
+    const dim3 cg((S + 255) / 256, rbs);
+    hipLaunchKernelGGL(k_nonce_colblk, cg, dim3(256), 0, st, tiles, S, (const unsigned long long *) tab, blk);
+    ZCHECK(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_nonce_colscan, cg, dim3(256), 0, st, tiles, S, tab, (const unsigned long long *) blk,
+                       ctx->send);
+    ZCHECK(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_nonce_frames, dim3(tiles), dim3(64), S * sizeof(unsigned long long), st, nn, T, S, sid,
+                       (const unsigned long long *) tab, w.nonce);
+    ZCHECK(ctx, hipGetLastError());
+    return 0;
+}
+
 // Multi-session replay prefix (k_fixup's excl) after the frame kernel: the
 // replay tables for up to kReplayMaxSessions sessions, else sort by session +
 // segmented scan (hipCUB).  Writes each session's new peer nonce (and its
@@ -1796,6 +1952,13 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
     if (e == hipSuccess)
         e = hipMemsetAsync(ctx->peer, 0, sizeof(unsigned long long) * max_sessions, ctx->own_stream);
     if (e == hipSuccess)
+        e = hipMalloc((void **) &ctx->send, sizeof(unsigned long long) * max_sessions);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_fill_u64, dim3((max_sessions + 255) / 256), dim3(256), 0, ctx->own_stream, ctx->send,
+                           max_sessions, 1ull);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
         e = hipStreamSynchronize(ctx->own_stream);
     if (e == hipSuccess)
         e = hipDeviceGetAttribute(&ctx->cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -1821,7 +1984,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     Workspace &w = ctx->ws;
     void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
                     w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.post, w.psnap, w.blockmax, w.zs,
-                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, w.rt, ctx->sessions, ctx->peer, ctx->dbuf};
+                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, w.rt, w.nonce, ctx->sessions, ctx->peer, ctx->send, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
             (void) hipFree(p);
@@ -1926,7 +2089,8 @@ int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], cons
     ZCHECK(ctx, hipMalloc((void **) &d, sizeof in));
     hipError_t e = hipMemcpyAsync(d, in, sizeof in, hipMemcpyHostToDevice, ctx->own_stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_session_setup, dim3(1), dim3(64), 0, ctx->own_stream, ctx->sessions, ctx->peer, sid, d);
+        hipLaunchKernelGGL(k_session_setup, dim3(1), dim3(64), 0, ctx->own_stream, ctx->sessions, ctx->peer, ctx->send,
+                           sid, d);
         e = hipGetLastError();
     }
     if (e == hipSuccess)
@@ -1936,30 +2100,51 @@ int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], cons
     return 0;
 }
 
-int zmqg_session_set_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t peer_nonce)
+// A session's u64 counter (peer nonce, send nonce), in order after the work
+// already issued on the ctx's last batch stream.
+static int session_u64_set(zmqg_ctx *ctx, unsigned long long *arr, uint32_t sid, uint64_t v)
 {
     if (!ctx || sid >= ctx->max_sessions)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    // in order after the batches already issued (on the ctx's last batch stream)
     hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->own_stream;
-    hipLaunchKernelGGL(k_set_peer, dim3(1), dim3(64), 0, st, ctx->peer, sid, (unsigned long long) peer_nonce);
+    hipLaunchKernelGGL(k_set_peer, dim3(1), dim3(64), 0, st, arr, sid, (unsigned long long) v);
     ZCHECK(ctx, hipGetLastError());
     ZCHECK(ctx, hipStreamSynchronize(st));
     return 0;
 }
 
-int zmqg_session_get_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *peer_nonce_out)
+static int session_u64_get(zmqg_ctx *ctx, const unsigned long long *arr, uint32_t sid, uint64_t *out)
 {
-    if (!ctx || sid >= ctx->max_sessions || !peer_nonce_out)
+    if (!ctx || sid >= ctx->max_sessions || !out)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->own_stream;
     unsigned long long v = 0;
-    ZCHECK(ctx, hipMemcpyAsync(&v, ctx->peer + sid, sizeof v, hipMemcpyDeviceToHost, st));
+    ZCHECK(ctx, hipMemcpyAsync(&v, arr + sid, sizeof v, hipMemcpyDeviceToHost, st));
     ZCHECK(ctx, hipStreamSynchronize(st));
-    *peer_nonce_out = v;
+    *out = v;
     return 0;
+}
+
+int zmqg_session_set_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t peer_nonce)
+{
+    return session_u64_set(ctx, ctx ? ctx->peer : nullptr, sid, peer_nonce);
+}
+
+int zmqg_session_get_peer_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *peer_nonce_out)
+{
+    return session_u64_get(ctx, ctx ? ctx->peer : nullptr, sid, peer_nonce_out);
+}
+
+int zmqg_session_set_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce)
+{
+    return session_u64_set(ctx, ctx ? ctx->send : nullptr, sid, nonce);
+}
+
+int zmqg_session_get_nonce(zmqg_ctx *ctx, uint32_t sid, uint64_t *nonce_out)
+{
+    return session_u64_get(ctx, ctx ? ctx->send : nullptr, sid, nonce_out);
 }
 
 uint64_t zmqg_wire_size(uint8_t msg_flags, int downgrade_sub, uint64_t payload_len)
@@ -1982,9 +2167,12 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
 {
     if (!ctx || check_n(n) || check_opts(opts))
         return -EINVAL;
+    const bool auto_nonce = opts && (opts->flags & ZMQG_OPT_NONCE_AUTO);
+    if (auto_nonce && ctx->max_sessions > kReplayMaxSessions)
+        return -EINVAL;
     if (n == 0)
         return 0;
-    if (!sid || !nonce || !flags || !in_off || !len || !in || !out_off || !out)
+    if (!sid || (!nonce && !auto_nonce) || !flags || !in_off || !len || !in || !out_off || !out)
         return -EINVAL;
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
@@ -2004,11 +2192,20 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     }
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
+    if (auto_nonce) {
+        if (ctx->max_sessions == 1) {
+            ctl.nonce_ctr = ctx->send; // in the frame kernel
+        } else {
+            if ((rc = nonce_multi(ctx, nn, sid, st)))
+                return rc;
+            nonce = w.nonce;
+        }
+    }
     ProfSpan main(ctx, ZMQG_PROF_ENCODE_MAIN, st);
     launch_frames<false>(G, nn, st, sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
                          ctx->max_sessions, nullptr, nullptr, ReplayOut{},
                          EncodeHead{sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
-                                    ctx->max_sessions, R},
+                                    ctx->max_sessions, R, ctl.nonce_ctr},
                          w.zs, ctl);
     ZCHECK(ctx, hipGetLastError());
     main.end();

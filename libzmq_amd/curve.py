@@ -56,12 +56,17 @@ _lib.zmqg_ctx_destroy.argtypes = [_P]
 _lib.zmqg_session_set.argtypes = [_P, _U32, _P, _P, _P, ctypes.c_int, _U64]
 _lib.zmqg_session_set_peer_nonce.argtypes = [_P, _U32, _U64]
 _lib.zmqg_session_get_peer_nonce.argtypes = [_P, _U32, ctypes.POINTER(_U64)]
+_lib.zmqg_session_set_nonce.argtypes = [_P, _U32, _U64]
+_lib.zmqg_session_get_nonce.argtypes = [_P, _U32, ctypes.POINTER(_U64)]
 _lib.zmqg_wire_size.argtypes = [ctypes.c_uint8, ctypes.c_int, _U64]
 _lib.zmqg_wire_size.restype = _U64
 _lib.zmqg_encode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
+OPT_NONCE_AUTO = 1  # zmqg_batch_opts.flags: encode nonces from the sessions' send counters
+
+
 class BatchOpts(ctypes.Structure):  # zmqg_batch_opts
-    _fields_ = [("size", _U32), ("reserved", _U32), ("max_len", _U64), ("status_out", _P),
+    _fields_ = [("size", _U32), ("flags", _U32), ("max_len", _U64), ("status_out", _P),
                 ("session_max_out", _P)]
 
 
@@ -94,7 +99,7 @@ _lib.zmqg_ctx_set_profiling.argtypes = [_P, ctypes.c_int]
 _lib.zmqg_ctx_get_profile.argtypes = [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
 _lib.zmqg_last_error.argtypes = [_P]
 _lib.zmqg_last_error.restype = ctypes.c_char_p
-assert _lib.zmqg_abi_version() == 2
+assert _lib.zmqg_abi_version() == 3
 
 
 def lib():
@@ -171,6 +176,15 @@ class CurveContext:
         self._check(_lib.zmqg_session_get_peer_nonce(self._ctx, sid, ctypes.byref(v)), "zmqg_session_get_peer_nonce")
         return v.value
 
+    def set_nonce(self, sid, nonce):
+        """The session's send counter (_cn_nonce) used by nonce_auto encodes."""
+        self._check(_lib.zmqg_session_set_nonce(self._ctx, sid, nonce), "zmqg_session_set_nonce")
+
+    def get_nonce(self, sid):
+        v = _U64(0)
+        self._check(_lib.zmqg_session_get_nonce(self._ctx, sid, ctypes.byref(v)), "zmqg_session_get_nonce")
+        return v.value
+
     # ---- profiling hooks (HIP events around the body kernels) ----
     # zmqg_curve.h ZMQG_PROF_*: MAIN = the frame kernel (dominant kernel),
     # CALL = the whole batch call, BODY = the chunked body kernel (big frames)
@@ -190,17 +204,19 @@ class CurveContext:
 
     # ---- device-resident batches (torch tensors on self.device) ----
     # max_len / status_out / session_max_out: zmqg_batch_opts (the _ex calls)
+    # nonce_auto: encode takes nonces from the sessions' send counters (nonce may be None)
     @staticmethod
-    def _opts(max_len, status_out, session_max_out):
-        if not max_len and status_out is None and session_max_out is None:
+    def _opts(max_len, status_out, session_max_out, nonce_auto=False):
+        if not max_len and status_out is None and session_max_out is None and not nonce_auto:
             return None
-        o = BatchOpts(ctypes.sizeof(BatchOpts), 0, int(max_len or 0), _ptr(status_out), _ptr(session_max_out))
+        o = BatchOpts(ctypes.sizeof(BatchOpts), OPT_NONCE_AUTO if nonce_auto else 0, int(max_len or 0),
+                      _ptr(status_out), _ptr(session_max_out))
         return ctypes.byref(o), o
 
     def encode_batch(self, sid, nonce, flags, in_off, length, inp, out_off, out, stream=None, max_len=0,
-                     status_out=None):
+                     status_out=None, nonce_auto=False):
         n = int(sid.numel())
-        o = self._opts(max_len, status_out, None)
+        o = self._opts(max_len, status_out, None, nonce_auto)
         self._check(_lib.zmqg_encode_batch_ex(self._ctx, n, _ptr(sid), _ptr(nonce), _ptr(flags), _ptr(in_off),
                                               _ptr(length), _ptr(inp), _ptr(out_off), _ptr(out),
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_encode_batch")

@@ -2,8 +2,8 @@
 // build (-DZMQG_SEQ_STAMPS=1): per wave, s_memtime at entry (0), before
 // window 0 (1), after it (2), at the start of step t (3+t) and after the
 // wait for step t's input words (24+t), after the loop (60), at the end
-// (61); for steps 1..7 also before the prefetch (44+t) and before the
-// stores (52+t).  Config-2 shape: 65,536 frames of 1 KiB, encode then decode.
+// (61); for steps 1..7 also after the input words are in (44+t), before the
+// stores (52+t) and after them (36+t).  Config-2 shape: 65,536 frames of 1 KiB, encode then decode.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DZMQG_SEQ_STAMPS=1 -o build/seq_stamps tools/seq_stamps.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -88,6 +88,7 @@ int main()
             if (t < 8) {
                 slots.push_back(44 + t);
                 slots.push_back(52 + t);
+                slots.push_back(36 + t);
             }
         }
         slots.push_back(60);
