@@ -41,6 +41,14 @@
 #define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: k_frames: 1 no Poly1305, 2 no stores, 4 no input shift; k_frames_seq: 8 no stores, 16 no loads, 32 no Salsa20, 64 no Poly1305
 #endif
 
+#ifndef ZMQG_SEQ_DEPTH
+#define ZMQG_SEQ_DEPTH 1 // k_frames_seq: windows of input in flight ahead of the one being processed (1 or 2)
+#endif
+
+#ifndef ZMQG_SEQ_PAIRST
+#define ZMQG_SEQ_PAIRST 0 // k_frames_seq: store windows in pairs
+#endif
+
 #ifndef ZMQG_FR_BS
 #define ZMQG_FR_BS 256 // frame-kernel workgroup size (threads)
 #endif
@@ -1136,6 +1144,13 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     // alternate between the two buffers
     uint32_t ddA[16], ddB[16];
     bool fastA = nw > 1u ? frame_prefetch(A4, lim, wave_end, 1u, ddA) : true, fastB = true;
+#if ZMQG_SEQ_DEPTH == 2
+    // two windows in flight: windows t, t+1, t+2 rotate through three buffers
+    uint32_t ddC[16];
+    bool fastC = true;
+    if (nw > 2u)
+        fastB = frame_prefetch(A4, lim, wave_end, 2u, ddB);
+#endif
 
     SEQ_STAMP(1u);
     // ---- step 0: window 0 (Poly1305 key, first 32 ciphertext bytes, header)
@@ -1225,6 +1240,9 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     // ---- steps 1 ..: window t (words in dd, prefetched by the previous
     // step; the two buffers alternate so that the loads keep their register
     // tuples)
+#if ZMQG_SEQ_PAIRST
+    uint32_t ysv[16], ysv_prev = 0; // an odd window's output, stored with the next one
+#endif
     auto step = [&](uint32_t t, uint32_t (&dd)[16], bool &fast, uint32_t (&dn)[16], bool &fastn) {
         SEQ_STAMP(3u + t);
         const bool act = t < nw;
@@ -1320,27 +1338,56 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             for (int k = 0; k < 16; ++k)
                 dn[k] = y[k] + k;
             fastn = true;
-        } else if (t + 1u < nw) {
-            fastn = frame_prefetch(A4, lim, wave_end, t + 1u, dn);
+        } else if (t + ZMQG_SEQ_DEPTH < nw) {
+            fastn = frame_prefetch(A4, lim, wave_end, t + ZMQG_SEQ_DEPTH, dn);
         }
         if (t < 8u)
             SEQ_STAMP(52u + t);
         if (ZMQG_FRAMES_ABLATE & 8) {
             if (act && y[3] == 0x12345678u && y[7] == ycarry)
                 *(GU32 *) (uintptr_t) B = y[0];
-        } else if (act) {
-            frame_store(B, t, S, y, ycarry, t + 1u == nw);
+        } else {
+#if ZMQG_SEQ_PAIRST
+            // windows go out in pairs (t-1, t at even t): a lane's 128
+            // contiguous bytes in consecutive instructions, so both halves of
+            // a 128-byte line reach L2 together
+            if ((t & 1u) && t + 1u < steps) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    ysv[k] = y[k];
+                ysv_prev = ycarry;
+            } else {
+                if ((t & 1u) == 0 && t - 1u < nw)
+                    frame_store(B, t - 1u, S, ysv, ysv_prev, t == nw);
+                if (act)
+                    frame_store(B, t, S, y, ycarry, t + 1u == nw);
+            }
+#else
+            if (act)
+                frame_store(B, t, S, y, ycarry, t + 1u == nw);
+#endif
         }
         ycarry = y[15];
         if (t < 8u)
             SEQ_STAMP(36u + t);
     };
+#if ZMQG_SEQ_DEPTH == 2
+#pragma unroll 1
+    for (uint32_t t = 1; t < steps; t += 3) {
+        step(t, ddA, fastA, ddC, fastC);
+        if (t + 1u < steps)
+            step(t + 1u, ddB, fastB, ddA, fastA);
+        if (t + 2u < steps)
+            step(t + 2u, ddC, fastC, ddB, fastB);
+    }
+#else
 #pragma unroll 1
     for (uint32_t t = 1; t < steps; t += 2) {
         step(t, ddA, fastA, ddB, fastB);
         if (t + 1u < steps)
             step(t + 1u, ddB, fastB, ddA, fastA);
     }
+#endif
     SEQ_STAMP(60u);
     // the last window's MAC
     if (steps > 0 && nw == steps)

@@ -44,6 +44,7 @@
 #include "curve_box.hpp"
 #include "curve_device.hpp"
 #include "curve_frames.hpp"
+#include "curve_frames_lds.hpp"
 #include "curve_z85.hpp"
 #include "curve_x25519.hpp"
 #include "curve_zmtp.hpp"
@@ -197,7 +198,7 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
-    int frames_cap[4] = {0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4, seq
+    int frames_cap[5] = {0, 0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4, seq, lds
     int force_g = -1;                 // ZMQG_FRAMES_G: frame-kernel variant override (experiments)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
@@ -1766,15 +1767,20 @@ struct ProfSpan {
     }
 };
 
-// Frame-kernel variant: 0 = one lane per frame (k_frames_seq: batches that
-// give every SIMD at least one wave), else G lanes per frame (k_frames) so
-// that a smaller batch still spreads over the chip.  ZMQG_FRAMES_G (0, 1, 2,
-// 4) forces a variant (experiments, tests).
+// Frame-kernel variant: one lane per frame once the batch gives every SIMD
+// a wave -- k_frames_lds (8: LDS-staged, coalesced traffic) when more than
+// one wave per SIMD is resident, k_frames_seq (0) at exactly one, where its
+// own loads and stores measured 4 % faster -- else G lanes per frame
+// (k_frames) so that a smaller batch still spreads over the chip.  Measured
+// per launch: 65,536 x 1 KiB seq 64 / lds 67 us;
+// 131,072 x 1 KiB seq 148-155 / lds 125-137 us; 262,144 x 1 KiB seq 293-328
+// / lds 264-276 us; 1 Mi x 256 B seq 382-469 / lds 363-429 us.
+// ZMQG_FRAMES_G (0, 1, 2, 4, 8) forces a variant (experiments, tests).
 int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 {
     if (ctx->force_g >= 0)
         return ctx->force_g;
-    return n >= 65536u ? 0 : n >= 32768u ? 2 : 4;
+    return n > 65536u ? 8 : n >= 65536u ? 0 : n >= 32768u ? 2 : 4;
 }
 
 // Workgroups of the decode frame kernel the device holds at once (occupancy
@@ -1782,10 +1788,11 @@ int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 // MI355X_MICROARCH.md, Residency), cached per variant.
 int frames_capacity(zmqg_ctx *ctx, int G)
 {
-    int &c = ctx->frames_cap[G == 0 ? 3 : G == 1 ? 0 : G == 2 ? 1 : 2];
+    int &c = ctx->frames_cap[G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0 : G == 2 ? 1 : 2];
     if (c == 0) {
         int nb = 0;
-        hipError_t e = G == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
+        hipError_t e = G == 8   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_lds<true, DecodeHead>, kFramesBS, 0)
+                       : G == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
                        : G == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
                        : G == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, kFramesBS, 0)
                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 4, DecodeHead>, kFramesBS, 0);
@@ -1800,7 +1807,13 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
                    const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
                    uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs, FrameCtl ctl)
 {
-    const dim3 grid((uint32_t) (((uint64_t) n * (G ? G : 1) + kFramesBS - 1) / kFramesBS));
+    const dim3 grid((uint32_t) (((uint64_t) n * (G == 1 || G == 2 || G == 4 ? G : 1) + kFramesBS - 1) / kFramesBS));
+    if (G == 8) {
+        hipLaunchKernelGGL((k_frames_lds<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
+                           out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
+                           ctl);
+        return;
+    }
     if (G == 0) {
         hipLaunchKernelGGL((k_frames_seq<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
                            out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
@@ -1933,7 +1946,7 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
     ctx->h_downgrade.assign(max_sessions, 0);
     if (const char *fg = getenv("ZMQG_FRAMES_G")) {
         const int g = atoi(fg);
-        if (g == 0 || g == 1 || g == 2 || g == 4)
+        if (g == 0 || g == 1 || g == 2 || g == 4 || g == 8)
             ctx->force_g = g;
     }
     hipError_t e = hipSetDevice(device);
@@ -2275,7 +2288,7 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         // A grid that fits the device at once can use blockIdx as the
         // look-back order (every workgroup becomes resident eventually,
         // whatever the dispatch order); a larger one takes tickets.
-        const uint64_t grid = ((uint64_t) nn * (G ? G : 1) + kFramesBS - 1) / kFramesBS;
+        const uint64_t grid = ((uint64_t) nn * (G == 1 || G == 2 || G == 4 ? G : 1) + kFramesBS - 1) / kFramesBS;
         rp.ordered = grid <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
     }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);

@@ -5,6 +5,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -13,7 +14,7 @@ for f in glob.glob(f"{sys.argv[1]}/**/*counter_collection.csv", recursive=True):
         name = r["Kernel_Name"]
         if "k_frames" not in name:
             continue
-        k = "k_frames<decode>" if "k_frames<true" in name else "k_frames<encode>"
+        k = "k_frames<decode>" if re.search(r"k_frames\w*<true", name) else "k_frames<encode>"
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
 for k, d in acc.items():

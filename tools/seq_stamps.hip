@@ -5,12 +5,23 @@
 // (61); for steps 1..7 also after the input words are in (44+t), before the
 // stores (52+t) and after them (36+t).  Config-2 shape: 65,536 frames of 1 KiB, encode then decode.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DZMQG_SEQ_STAMPS=1 -o build/seq_stamps tools/seq_stamps.hip
+// (add -DSTAMP_LDS=1 for k_frames_lds: slots 3+t step start, 44+t after the
+// wait, 52+t after the DMA and store issue, 24+t after keystream and MAC,
+// 36+t after the ring write)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <vector>
 #include <algorithm>
-#include "../libzmq_amd/csrc/curve_frames.hpp"
+#include "../libzmq_amd/csrc/curve_frames_lds.hpp"
+#ifndef STAMP_LDS
+#define STAMP_LDS 0 // 1: stamp k_frames_lds instead of k_frames_seq
+#endif
+#if STAMP_LDS
+#define KFR k_frames_lds
+#else
+#define KFR k_frames_seq
+#endif
 using namespace zmqg;
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
@@ -68,11 +79,11 @@ int main()
             CHECK(hipMemset(d_clk, 0, 8 * 64 * nwaves));
             rp.clk = rep == 2 ? d_clk : nullptr;
             if (!dec)
-                hipLaunchKernelGGL((k_frames_seq<false, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid, d_nonce,
+                hipLaunchKernelGGL((KFR<false, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid, d_nonce,
                                    d_flags, d_ioff, d_len, d_pay, d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr,
                                    nullptr, rp, NoBigFrames{}, d_zs, FrameCtl{});
             else
-                hipLaunchKernelGGL((k_frames_seq<true, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid,
+                hipLaunchKernelGGL((KFR<true, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid,
                                    (const uint64_t *) nullptr, (const uint8_t *) nullptr, d_ooff, d_wl, d_wire, d_ioff,
                                    d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, NoBigFrames{}, d_zs, FrameCtl{});
             CHECK(hipDeviceSynchronize());
@@ -81,18 +92,22 @@ int main()
         CHECK(hipMemcpy(c.data(), d_clk, 8 * 64 * nwaves, hipMemcpyDeviceToHost));
         // per slot: median over waves of (stamp - entry stamp), and of step deltas
         printf("%s: median cycles since entry per phase (min/median/max over waves)\n", dec ? "decode" : "encode");
-        std::vector<int> slots = {1, 2};
-        for (int t = 1; t <= 16; ++t) {
-            slots.push_back(3 + t);
-            slots.push_back(24 + t);
-            if (t < 8) {
-                slots.push_back(44 + t);
-                slots.push_back(52 + t);
-                slots.push_back(36 + t);
-            }
+        // every stamped slot, in order of its median time
+        std::vector<std::pair<long long, int>> order;
+        for (int sl = 1; sl < 64; ++sl) {
+            std::vector<long long> v;
+            for (size_t w = 0; w < nwaves; ++w)
+                if (c[64 * w + sl])
+                    v.push_back((long long) (c[64 * w + sl] - c[64 * w]));
+            if (v.empty())
+                continue;
+            std::sort(v.begin(), v.end());
+            order.push_back({v[v.size() / 2], sl});
         }
-        slots.push_back(60);
-        slots.push_back(61);
+        std::sort(order.begin(), order.end());
+        std::vector<int> slots;
+        for (auto &o : order)
+            slots.push_back(o.second);
         for (int sl : slots) {
             std::vector<long long> v;
             for (size_t w = 0; w < nwaves; ++w)
