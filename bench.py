@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-staged", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of CPU baseline sampling")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the other BASELINE configs (3, 4, 5) measured after the main line")
+    p.add_argument("--configs", default="3,4,5", help="which of the other BASELINE configs to measure")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from the host instead of replaying the captured K steps as one hipGraph")
     return p.parse_args()
@@ -263,6 +266,9 @@ def main():
         "roofline": roofline,
     }
 
+    if not args.no_configs:
+        result["configs"] = other_configs(C, torch, dev, local, rank, world, args.configs.split(","))
+
     if rank == 0 and world == 1 and not args.no_host_staged:
         result["host_paths"] = host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_off, lens,
                                           out_off, wlen, n, P, W)
@@ -275,6 +281,103 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def config_batches(which, rank, world):
+    """Per-rank share of BASELINE configs 3-5: (name, sizes, sessions, scaling, note).
+    Config 3 is one GPU's batch (run on every rank: weak); configs 4 and 5
+    split one batch over the ranks with shard.partition (strong scaling),
+    each session's frames on one rank, so there is no exchange."""
+    from libzmq_amd import shard
+    if which == "3":
+        rng = np.random.default_rng(3 + rank)
+        return ("config3: 49,152 frames of {64 B, 1 KiB, 64 KiB}, 256 sessions per GPU",
+                rng.choice([64, 1024, 65536], 49152).astype(np.int64), 256, "weak")
+    if which == "4":
+        n_all, size, S = 16 << 20, 256, 1024
+    elif which == "5":
+        n_all, size, S = 1 << 10, 16 << 20, 8
+    else:
+        raise ValueError(which)
+    lo, hi = shard.partition(shard.stream_blocks(np.full(n_all, 33 + size, np.int64)), world)[rank]
+    name = ("config4: 16 Mi x 256 B frames, 1024 sessions, split over the GPUs" if which == "4" else
+            "config5: 1 Ki x 16 MiB frames, 8 sessions, split over the GPUs")
+    return name, np.full(hi - lo, size, np.int64), max(1, S // world), "strong"
+
+
+def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1):
+    """BASELINE configs 3, 4, 5: encode (device-assigned nonces) + decode round
+    trips of device-resident batches, every result checked, timed like the
+    main line (barrier + synchronize, max over ranks); payload GiB/s of the
+    whole job."""
+    import torch.distributed as dist
+    from libzmq_amd import shard
+    out = {}
+    for w in which:
+        name, sizes, S, scaling = config_batches(w, rank, world)
+        n = len(sizes)
+        g = torch.Generator(device=dev)
+        g.manual_seed(0xC0 + 7 * rank + int(w))
+        enc, dec = C.CurveContext(local, S), C.CurveContext(local, S)
+        rng = np.random.default_rng(0xC0 + rank)
+        for s in range(S):
+            k = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+            enc.session_set(s, k, C.CLIENT_PREFIX, C.SERVER_PREFIX)
+            enc.set_nonce(s, 3)
+            dec.session_set(s, k, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+        t = lambda a, d: torch.from_numpy(np.ascontiguousarray(a).view(d)).to(dev)
+        in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        W = sizes + 33
+        out_off = np.concatenate([[0], np.cumsum(W)[:-1]]).astype(np.uint64)
+        sid = (np.arange(n) * S // max(n, 1)).astype(np.uint32)  # a connection's frames together
+        d_sid, d_in, d_out = t(sid, np.int32), t(in_off, np.int64), t(out_off, np.int64)
+        d_len, d_wl = t(sizes.astype(np.uint32), np.int32), t(W.astype(np.uint32), np.int32)
+        flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+        total = int(sizes.sum())
+        payload = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+        wire = torch.empty(int(W.sum()), dtype=torch.uint8, device=dev)
+        back = torch.empty(total, dtype=torch.uint8, device=dev)
+        fl = torch.empty(n, dtype=torch.uint8, device=dev)
+        st = torch.empty(n, dtype=torch.int32, device=dev)
+        ml = int(sizes.max())
+        bound = ml if ml + 43 <= 4608 else 0  # the frame kernel's range: skip the large-frame launches
+
+        def step():
+            enc.encode_batch(d_sid, None, flags, d_in, d_len, payload, d_out, wire, max_len=bound, nonce_auto=True)
+            dec.decode_batch(d_sid, d_out, d_wl, wire, d_in, back, fl, st, max_len=bound + 33 if bound else 0)
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        dt = shard.max_over_ranks(time.perf_counter() - t0)
+        ok = int((st != 0).sum()) == 0 and torch.equal(back, payload)
+        oks = shard.max_over_ranks(0.0 if ok else 1.0) == 0.0
+        assert oks, f"config {w}: round trip mismatch"
+        job_bytes = total * world if scaling == "weak" else sum_over_ranks(total)
+        job_frames = n * world if scaling == "weak" else sum_over_ranks(n)
+        out["config" + w] = {"workload": name, "scaling": scaling, "value": job_bytes / 2**30 * steps / dt,
+                             "unit": "GiB/s", "msgs_per_s": job_frames * steps / dt, "ms_per_step": 1e3 * dt / steps,
+                             "frames_per_gpu": n, "sessions_per_gpu": S, "steps": steps, "warmup": warmup,
+                             "checked": "every frame: status 0, decoded payload == input"}
+        del payload, wire, back, enc, dec
+        torch.cuda.empty_cache()
+    return out
+
+
+def sum_over_ranks(v):
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(v)
+    x = torch.tensor([float(v)], dtype=torch.float64)
+    dist.all_reduce(x)
+    return float(x.item())
 
 
 def host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_off, lens, out_off, wlen, n, P, W):

@@ -57,19 +57,37 @@ def header_nonces(wire, in_off, wire_len):
     """Header-valid nonce of each wire frame (0 where the header fails), the
     value the replay rule compares: check_basic_command_structure
     (src/mechanism_base.cpp:14-25), "\\x07MESSAGE" and size >= 33
-    (src/curve_mechanism_base.cpp:80-97), nonce = big-endian bytes 8..15."""
+    (src/curve_mechanism_base.cpp:80-97), nonce = big-endian bytes 8..15.
+    Host arrays, vectorised (a gather of 16 bytes per frame); on the device
+    the same values come from CurveContext.session_max_batch /
+    decode_batch(session_max_out=...) (include/zmqg_curve.h)."""
     buf = np.asarray(wire, np.uint8)
     off = np.asarray(in_off, np.int64)
     wl = np.asarray(wire_len, np.int64)
     out = np.zeros(len(off), np.uint64)
-    for i, (o, l) in enumerate(zip(off, wl)):
-        if l < 33:
-            continue
-        f = buf[o:o + 16].tobytes()
-        if l <= f[0] or f[:8] != MESSAGE_HDR:
-            continue
-        out[i] = int.from_bytes(f[8:16], "big")
+    if len(off) == 0:
+        return out
+    ok = wl >= 33
+    idx = np.minimum(off[:, None] + np.arange(16)[None, :], max(len(buf) - 1, 0))
+    h = buf[idx]  # [n, 16]; rows of frames shorter than 33 bytes are ignored below
+    ok &= wl > h[:, 0]
+    ok &= (h[:, :8] == np.frombuffer(MESSAGE_HDR, np.uint8)[None, :]).all(axis=1)
+    be = h[:, 8:16].astype(np.uint64)
+    v = np.zeros(len(off), np.uint64)
+    for k in range(8):  # big-endian bytes 8..15
+        v = (v << np.uint64(8)) | be[:, k]
+    out[ok] = v[ok]
     return out
+
+
+def session_max_device(ctx, sid, in_off, wire_len, wire, n_sessions, stream=None):
+    """Per-session maxima of header-valid nonces computed on the device
+    (zmqg_session_max_batch): device tensors in, a host uint64 vector out."""
+    import torch
+    m = torch.zeros(n_sessions, dtype=torch.int64, device=wire.device)
+    ctx.session_max_batch(sid, in_off, wire_len, wire, m, stream)
+    torch.cuda.synchronize(wire.device)
+    return m.cpu().numpy().view(np.uint64)
 
 
 def session_max(sid, nonces, n_sessions):

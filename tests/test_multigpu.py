@@ -152,3 +152,23 @@ def test_header_nonces_follow_check_validity():
     wl = np.array([len(f) for f in frames], np.uint32)
     v = shard.header_nonces(inp, off, wl)
     assert list(v) == [1234, 0, 0, 1234, 0]
+
+
+def test_header_nonces_vectorised_matches_rule():
+    """shard.header_nonces (vectorised) against the header rule written as a
+    per-frame loop: size >= 33, size > data[0] (mechanism_base.cpp:14-25),
+    "\\x07MESSAGE" prefix (curve_mechanism_base.cpp:85-90), BE nonce."""
+    rng = np.random.default_rng(11)
+    frames = []
+    for _ in range(400):
+        f = bytearray(rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes())
+        if len(f) >= 8 and rng.random() < 0.7:
+            f[:8] = b"\x07MESSAGE"
+        frames.append(bytes(f))
+    inp, in_off = pack(frames)
+    wl = np.array([len(f) for f in frames], np.int64)
+    got = shard.header_nonces(inp, in_off, wl)
+    exp = [0 if len(f) < 33 or len(f) <= f[0] or f[:8] != b"\x07MESSAGE" else int.from_bytes(f[8:16], "big")
+           for f in frames]
+    assert np.array_equal(got, np.array(exp, np.uint64))
+    assert (got != 0).sum() > 50
