@@ -40,7 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-ROOF_KERNEL = "k_frames<decode>"  # the dominant kernel of the bench workload
+ROOF_KERNEL = "k_frames_seq<decode>"  # the dominant kernel of the bench workload (one lane per frame)
 
 
 def parse():

@@ -277,9 +277,12 @@ int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
  * decoded frame (msg_t::set_flags ORs, src/msg.cpp:433-436).  result:
  * frames returned, bytes of `in` they cover (an incomplete last frame is
  * left for the next call), payload bytes written, and error = EMSGSIZE when
- * a frame's size exceeds max_msg_size (>= 0; -1 = no limit) or 2^32 - 1,
- * where the reference decoder fails (src/v2_decoder.cpp:74-84): the frames
- * before it are returned.  A complete frame that is not a MESSAGE command
+ * a frame's size exceeds max_msg_size (>= 0; -1 = no limit), where the
+ * reference decoder fails (src/v2_decoder.cpp:74-84): the frames before it
+ * are returned.  A size above 2^32 - 1 also ends the parse with EMSGSIZE:
+ * that is a restriction of this library (frame lengths are 32-bit), not
+ * reference behaviour -- on LP64 the reference's size_t check
+ * (src/v2_decoder.cpp:78) never fires and it would accept such a frame.  A complete frame that is not a MESSAGE command
  * is returned as the last frame, with the status the mechanism gives it;
  * the reference's engine stops at the first failing frame, and so should
  * the caller.  Arrays hold max_frames entries; `out` at least in_bytes.

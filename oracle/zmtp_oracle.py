@@ -47,6 +47,9 @@ def parse(buf, max_msg_size=-1, max_frames=None):
             size, hdr = struct.unpack(">Q", buf[pos + 1:pos + 9])[0], 9
         else:
             size, hdr = buf[pos + 1], 2
+        # max_msg_size: src/v2_decoder.cpp:74-84.  The 2^32 - 1 bound is this
+        # library's restriction (32-bit frame lengths, include/zmqg_curve.h),
+        # not the reference's: on LP64 its size_t check (:78) never fires.
         if (max_msg_size >= 0 and size > max_msg_size) or size > 0xFFFFFFFF:
             error = EMSGSIZE
             break

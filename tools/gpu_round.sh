@@ -26,6 +26,6 @@ if [[ $MODE == all || $MODE == bench ]]; then
   step bench 600 python bench.py --steps 50 --warmup 10
 fi
 if [[ $MODE == all || $MODE == prof ]]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-staged
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-staged --no-configs
 fi
 exit 0

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""profiles/pmc_valu_config2.json and profiles/pmc_traffic_config2.json from
+the PMC passes of tools/pmc_profiles.sh (gpurun_out/pmcv, gpurun_out/pmct):
+per-launch VALU/SALU/VMEM wave-instruction counts and HBM bytes of the
+config-2 frame kernels, FETCH_SIZE scaled by the calibration copy of the same
+access shape (tools/framecopy.hip, LANE, one window in flight)."""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+N, P = 65536, 1024
+
+
+def per_kernel(d):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return acc
+
+
+def pick(acc, pat, counter):
+    for k, v in acc.items():
+        if re.search(pat, k) and counter in v:
+            return sum(v[counter]) / len(v[counter]), k
+    raise KeyError(pat)
+
+
+valu = json.load(open(f"{root}/pmcv/summary.json"))
+fetch, write = per_kernel(f"{root}/pmct/fetch"), per_kernel(f"{root}/pmct/write")
+fcal, wcal = per_kernel(f"{root}/pmct/fetch_cal"), per_kernel(f"{root}/pmct/write_cal")
+cal_f, _ = pick(fcal, r"k_copy<false, 1>", "FETCH_SIZE")
+cal_w, _ = pick(wcal, r"k_copy<false, 1>", "WRITE_SIZE")
+moved_kib = N * P / 1024
+scale = moved_kib / cal_f
+out_t, out_v = {}, {}
+for dec in (True, False):
+    tag = "decode" if dec else "encode"
+    pat = r"k_frames\w*<%s" % ("true" if dec else "false")
+    f, kname = pick(fetch, pat, "FETCH_SIZE")
+    w, _ = pick(write, pat, "WRITE_SIZE")
+    kshort = re.search(r"(k_frames\w*)<", kname).group(1) + "<%s>" % tag
+    alg_r = N * (P + 49) if dec else N * (P + 25)
+    alg_w = N * (P + 5) if dec else N * (P + 33)
+    t = {"kernel": kshort, "read_bytes_per_launch": f * scale * 1024, "write_bytes_per_launch": w * 1024,
+         "fetch_size_kib_raw": f, "write_size_kib_raw": w, "algorithmic_read_bytes_per_launch": alg_r,
+         "algorithmic_write_bytes_per_launch": alg_w}
+    v = valu["k_frames<%s>" % tag]
+    vv = {"kernel": kshort, "valu_wave_instr_per_launch": v["SQ_INSTS_VALU"], "salu_instr_per_launch": v["SQ_INSTS_SALU"],
+          "vmem_instr_per_launch": v["SQ_INSTS_VMEM"], "waves": v["SQ_WAVES"],
+          "valu_lane_ops_per_frame": v["SQ_INSTS_VALU"] * 64 / N}
+    if dec:
+        out_t.update(t)
+        out_v.update(vv)
+    else:
+        out_t["encode"] = t
+        out_v["encode"] = vv
+out_t.update({
+    "workload": "config2: 65536 x 1024 B frames, one session, one lane per frame (1024 waves, 1 per SIMD)",
+    "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace) of python bench.py "
+              "--eager --steps 3 --warmup 1 (tools/pmc_traffic.sh via tools/pmc_profiles.sh); calibration: the same "
+              "counters over tools/framecopy (65536 x 1024 B, LANE shape, known bytes); tools/pmc_profiles.py",
+    "units": "bytes per launch", "fetch_scale": scale,
+    "fetch_scale_note": "FETCH_SIZE under-reports this access shape on gfx950 (MI355X_MICROARCH.md HBM section): "
+                        "the calibration copy reads %.0f KiB reported per %.0f KiB moved, so reads are scaled by "
+                        "%.3f.  WRITE_SIZE is taken as reported; the calibration copy's lane stores show %.2fx "
+                        "the bytes moved (partial-line writes), the same kind of amplification as the frame kernel."
+                        % (cal_f, moved_kib, scale, cal_w / moved_kib)})
+out_v.update({
+    "workload": out_t["workload"],
+    "source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES "
+              "--kernel-trace of python bench.py --eager --steps 3 --warmup 1 (tools/pmc_valu_bench.sh)",
+    "units": "wave instructions per launch (one VALU wave instruction = 64 lane operations; a wave alone on its "
+             "SIMD issues one every 4 cycles)",
+    "salsa20_lane_ops_per_frame_floor": 17 * 940,
+    "simds": 1024, "lanes_per_simd_per_cycle": 16, "clock_ghz_spec": 2.4, "clock_ghz_measured": 2.09,
+    "clock_note": "s_memtime over s_memrealtime per workgroup of the frame kernel (tools/frames_bench.hip): "
+                  "2.05-2.12 GHz per XCD under this load",
+    "peak_note": "16 lanes per cycle per SIMD: one wave per SIMD issues a VALU instruction every 4 cycles, and the "
+                 "Salsa20 instruction mix issues at that rate at every occupancy (profiles/valu_rates_r02.md)"})
+json.dump(out_t, open("profiles/pmc_traffic_config2.json", "w"), indent=1)
+json.dump(out_v, open("profiles/pmc_valu_config2.json", "w"), indent=1)
+print(json.dumps({"traffic": {k: out_t[k] for k in ("kernel", "read_bytes_per_launch", "write_bytes_per_launch")},
+                  "valu": {k: out_v[k] for k in ("kernel", "valu_wave_instr_per_launch", "valu_lane_ops_per_frame")}}))
