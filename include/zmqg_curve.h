@@ -285,8 +285,16 @@ int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
  * (src/v2_decoder.cpp:78) never fires and it would accept such a frame.  A complete frame that is not a MESSAGE command
  * is returned as the last frame, with the status the mechanism gives it;
  * the reference's engine stops at the first failing frame, and so should
- * the caller.  Arrays hold max_frames entries; `out` at least in_bytes.
- * Returns after the stream has synchronised.  in_bytes < 2^31. */
+ * the caller.  Arrays hold max_frames entries (entries from result.frames
+ * on hold empty frames: length 0, a malformed status); `out` at least
+ * in_bytes.  Returns after the stream has synchronised: the result is the
+ * call's only read back (the frame count stays on the device; the decode
+ * runs over max_frames).  in_bytes < 2^31.
+ *
+ * zmqg_decode_zmtp_async: the same, without synchronising: `result` must be
+ * device-accessible (device memory, or pinned host memory from
+ * zmqg_host_alloc) and holds the result once the stream reaches this point
+ * (zmqg_fence_record / _query). */
 typedef struct zmqg_zmtp_result {
     uint64_t frames;
     uint64_t consumed;
@@ -301,6 +309,10 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
                      uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
                      uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result,
                      void *stream);
+int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
+                           uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
+                           uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result,
+                           void *stream);
 
 /* Handshake key derivation in batches, one
  * 32-byte item per thread, items packed back to back:

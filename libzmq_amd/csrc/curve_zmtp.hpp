@@ -14,18 +14,23 @@
 // byte, a 1- or 8-byte size (LARGE), checks the size against maxmsgsize
 // (EMSGSIZE) and takes the body.  Frame boundaries are a sequential chain
 // (each size locates the next frame), so the device finds them without
-// walking byte by byte:
+// walking byte by byte, and without the host reading anything back until the
+// call's result:
 //   1. candidates: every offset p whose header and body lie inside the
 //      buffer, whose size passes maxmsgsize, and whose body starts with
 //      "\x07MESSAGE" -- a superset of the true MESSAGE frame starts (a
-//      peer can plant the signature inside a body), in offset order, less
-//      the shadow a LARGE header's size field casts (k_zmtp_scan);
+//      peer can plant the signature inside a body) -- less the shadow a
+//      LARGE header's size field casts; gathered per 16 KiB workgroup in
+//      stream order and concatenated (k_zmtp_scan, k_zmtp_compact);
 //   2. links: candidate k is linked when the frame at cand[k] ends exactly
-//      at cand[k+1]; the unlinked ones are listed (normally just the last);
+//      at cand[k+1]; each candidate learns the next unlinked one
+//      (k_zmtp_links, k_zmtp_segnext; normally only the last is unlinked);
 //   3. one thread walks the chain from offset 0 over whole linked runs,
 //      jumping only at unlinked candidates (a binary search for the next
 //      frame's offset among the candidates), and records the runs;
-//   4. one thread per candidate turns the runs into frame descriptors.
+//   4. one thread per candidate turns the runs into frame descriptors, and
+//      the entries up to max_frames into empty frames, so the decode runs
+//      over max_frames with the frame count left on the device.
 // A clean stream costs two parallel passes and a one-step walk; planted
 // signatures add one binary search per frame that carries one.  The frame
 // after the chain decides the rest, as the reference decoder would: a
@@ -91,111 +96,288 @@ struct ZmtpIsCandidate {
     }
 };
 
-// Candidate scan, one thread per 16 aligned bytes: every 0x07 byte q that
-// starts "\x07MESSAGE" is a body start; the frame starts it can belong to
-// are q-9 (LARGE header) and q-2 (short header).  A LARGE frame's size field
-// ends "<b7> <b8>" right before its body, so whenever <b7> has no LARGE bit
-// q-2 also reads as a short header (size <b8>) with the same signature: a
-// shadow inside the true frame's header.  When q-9 is a candidate, q-2 is
-// therefore dropped.  (A true frame never starts inside another true frame's
-// header; a planted LARGE candidate at q-9 whose header covers a true start
-// at q-2 only ends the walk early: that frame is then taken as the frame
-// after the chain, and the next call resumes behind it.)  Candidates are
-// appended unordered; the caller sorts them.
-constexpr int kZmtpScanIters = 16;  // 16-byte chunks per thread: 64 KB per workgroup
-constexpr int kZmtpScanList = 1024; // candidates a workgroup gathers in LDS before one global reservation
+// Candidate scan (k_zmtp_scan): one workgroup per 16 KiB of the stream, in
+// chunks of 16 bytes, consecutive lanes on consecutive chunks.  Every 0x07 byte q that starts "\x07MESSAGE"
+// is a body start; the frame starts it can belong to are q-9 (LARGE header)
+// and q-2 (short header).  A LARGE frame's size field ends "<b7> <b8>" right
+// before its body, so whenever <b7> has no LARGE bit q-2 also reads as a
+// short header (size <b8>) with the same signature: a shadow inside the true
+// frame's header.  When q-9 is a candidate, q-2 is therefore dropped.  (A
+// true frame never starts inside another true frame's header; a planted LARGE
+// candidate at q-9 whose header covers a true start at q-2 only ends the walk
+// early: that frame is then taken as the frame after the chain, and the next
+// call resumes behind it.)
+// Ordering: signatures are at least 8 bytes apart (0x07 does not occur in
+// "MESSAGE"), so a candidate's offset orders like its signature's, and a
+// workgroup's candidates, written in thread order after a block scan of the
+// threads' counts, are sorted; the workgroups' lists, concatenated in
+// workgroup order (k_zmtp_compact), are the sorted candidate array -- no sort
+// and no count read back by the host.
+constexpr uint32_t kZmtpThreads = 256;
+constexpr uint32_t kZmtpWgBytes = 64u * kZmtpThreads;    // 16 KiB of stream per workgroup
+constexpr uint32_t kZmtpWgCap = kZmtpWgBytes / 8u;         // candidates a workgroup can hold
+constexpr unsigned long long kZmtpNone = ~0ull;
 
-__device__ __forceinline__ void zmtp_emit(uint64_t p, uint64_t *list, uint32_t *lcount, uint64_t *cand,
-                                          unsigned long long *count)
+// exclusive sum over the workgroup's threads (256); total to every thread
+__device__ __forceinline__ uint32_t zmtp_block_excl(uint32_t v, uint32_t &total)
 {
-    const uint32_t k = atomicAdd(lcount, 1u);
-    if (k < (uint32_t) kZmtpScanList)
-        list[k] = p;
-    else
-        cand[atomicAdd(count, 1ull)] = p; // overflow (a flood of planted signatures): one by one
+    __shared__ uint32_t sh[kZmtpThreads / 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t) __shfl_up((int) x, d);
+        if ((int) lane >= d)
+            x += o;
+    }
+    if (lane == 63)
+        sh[wv] = x;
+    __syncthreads();
+    uint32_t base = 0;
+    total = 0;
+    for (uint32_t k = 0; k < kZmtpThreads / 64; ++k) {
+        if (k < wv)
+            base += sh[k];
+        total += sh[k];
+    }
+    __syncthreads();
+    return base + x - v;
 }
 
-__global__ __launch_bounds__(256) void k_zmtp_scan(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_t *cand,
-                                                   unsigned long long *count)
+// byte o (static) of a little-endian register window
+template <int O, int NW>
+__device__ __forceinline__ uint32_t zmtp_byte(const uint32_t (&w)[NW])
 {
-    // a contended global counter takes ~88 returning atomics per us, so
-    // candidates are gathered per workgroup and reserved with one atomic
-    __shared__ uint64_t list[kZmtpScanList];
-    __shared__ uint32_t lcount;
-    __shared__ unsigned long long gbase;
-    if (threadIdx.x == 0)
-        lcount = 0;
-    __syncthreads();
-    const ZmtpIsCandidate isc{b, n, max_msg};
-    const uint64_t wg0 = (uint64_t) blockIdx.x * blockDim.x * 16u * kZmtpScanIters;
-    for (int it = 0; it < kZmtpScanIters; ++it) {
-        const uint64_t base = wg0 + ((uint64_t) it * blockDim.x + threadIdx.x) * 16u;
-        if (base >= n)
-            break;
-        uint32_t w[4];
-        if (base + 16 <= n) {
-            const uint4 v = *(const uint4 *) (b + base);
-            w[0] = v.x;
-            w[1] = v.y;
-            w[2] = v.z;
-            w[3] = v.w;
+    static_assert(O >= 0 && O / 4 < NW, "byte inside the window");
+    return (w[O / 4] >> (8 * (O % 4))) & 0xffu;
+}
+
+// The candidate for a "\x07MESSAGE" at stream offset qq, whose byte is at
+// offset O of the register window w (which holds the 16 bytes before the
+// chunk too): the frame start it belongs to -- qq-9 (LARGE header) or qq-2
+// (short) -- when that header passes ZmtpIsCandidate's tests, else none.
+// Header bytes come from the registers: no memory access.
+template <int O, int NW>
+__device__ __forceinline__ uint64_t zmtp_cand_at(const uint32_t (&w)[NW], uint64_t qq, uint64_t n, int64_t max_msg)
+{
+    if (qq >= 9 && (zmtp_byte<O - 9>(w) & kZmtpLarge)) {
+        uint64_t size = 0;
+        size = (size << 8) | zmtp_byte<O - 8>(w);
+        size = (size << 8) | zmtp_byte<O - 7>(w);
+        size = (size << 8) | zmtp_byte<O - 6>(w);
+        size = (size << 8) | zmtp_byte<O - 5>(w);
+        size = (size << 8) | zmtp_byte<O - 4>(w);
+        size = (size << 8) | zmtp_byte<O - 3>(w);
+        size = (size << 8) | zmtp_byte<O - 2>(w);
+        size = (size << 8) | zmtp_byte<O - 1>(w);
+        const uint64_t p = qq - 9;
+        if (zmtp_size_ok(size, max_msg) && size >= 8 && size <= n - p - 9)
+            return p;
+    }
+    if (qq >= 2 && !(zmtp_byte<O - 2>(w) & kZmtpLarge)) {
+        const uint64_t size = zmtp_byte<O - 1>(w), p = qq - 2;
+        if (zmtp_size_ok(size, max_msg) && size >= 8 && size <= n - p - 2)
+            return p;
+    }
+    return kZmtpNone;
+}
+
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, uint64_t n, int64_t max_msg,
+                                                            uint64_t *cand_wg, uint64_t *count_wg)
+{
+    // Chunk r of the workgroup (16 bytes, r = 256 k + thread): consecutive
+    // lanes read consecutive chunks (coalesced), with the 16 bytes before the
+    // chunk (a header) and the 8 after (a signature's tail), so the signature
+    // and header tests run on registers.  Candidates go out in chunk order: a
+    // block scan of the counts per k.
+    const uint64_t wg0 = (uint64_t) blockIdx.x * kZmtpWgBytes;
+    uint32_t base_out = 0;
+    uint64_t *const dst0 = cand_wg + (size_t) blockIdx.x * kZmtpWgCap;
+#pragma unroll 1
+    for (uint32_t k = 0; k < kZmtpWgBytes / 16u / kZmtpThreads; ++k) {
+        const uint64_t base = wg0 + 16ull * (k * kZmtpThreads + threadIdx.x);
+        uint32_t w[10]; // stream bytes [base - 16, base + 24), zero outside [0, n)
+        if (base >= 16 && base + 24 <= n) {
+            const uint4 v0 = *(const uint4 *) (b + base - 16);
+            const uint4 v1 = *(const uint4 *) (b + base);
+            const uint2 v2 = *(const uint2 *) (b + base + 16);
+            w[0] = v0.x;
+            w[1] = v0.y;
+            w[2] = v0.z;
+            w[3] = v0.w;
+            w[4] = v1.x;
+            w[5] = v1.y;
+            w[6] = v1.z;
+            w[7] = v1.w;
+            w[8] = v2.x;
+            w[9] = v2.y;
         } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int q = 0; q < 10; ++q) {
                 uint32_t x = 0;
                 for (int j = 0; j < 4; ++j) {
-                    const uint64_t p = base + 4 * k + j;
-                    x |= (uint32_t) (p < n ? b[p] : 0u) << (8 * j);
+                    const int64_t p = (int64_t) base - 16 + 4 * q + j;
+                    x |= (uint32_t) (p >= 0 && (uint64_t) p < n ? b[p] : 0u) << (8 * j);
                 }
-                w[k] = x;
+                w[q] = x;
             }
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t x = w[k] ^ 0x07070707u;
-            if (!((x - 0x01010101u) & ~x & 0x80808080u))
-                continue; // no 0x07 byte in this word
-            for (int j = 0; j < 4; ++j) {
-                if (((w[k] >> (8 * j)) & 0xffu) != 0x07u)
-                    continue;
-                const uint64_t q = base + 4 * k + j;
-                if (q + 8 > n || b[q + 1] != 'M' || b[q + 2] != 'E' || b[q + 3] != 'S' || b[q + 4] != 'S' ||
-                    b[q + 5] != 'A' || b[q + 6] != 'G' || b[q + 7] != 'E')
-                    continue;
-                if (q >= 9 && (b[q - 9] & kZmtpLarge) && isc(q - 9))
-                    zmtp_emit(q - 9, list, &lcount, cand, count);
-                else if (q >= 2 && !(b[q - 2] & kZmtpLarge) && isc(q - 2))
-                    zmtp_emit(q - 2, list, &lcount, cand, count);
-            }
-        }
+        uint64_t found[2];
+        uint32_t cnt = 0;
+        auto at = [&](uint64_t p) {
+            if (p != kZmtpNone && cnt < 2u)
+                found[cnt++] = p; // (at most 2: signatures are >= 8 bytes apart)
+        };
+#define ZMTP_SIG(Q, J)                                                                                           \
+    if (__builtin_amdgcn_alignbyte(w[5 + Q], w[4 + Q], J) == 0x53454d07u &&                                      \
+        __builtin_amdgcn_alignbyte(w[6 + Q], w[5 + Q], J) == 0x45474153u && base + 4 * Q + J + 8 <= n)           \
+        at(zmtp_cand_at<16 + 4 * Q + J>(w, base + 4 * Q + J, n, max_msg));
+#define ZMTP_WORD(Q)                                                                                             \
+    {                                                                                                            \
+        const uint32_t x = w[4 + Q] ^ 0x07070707u;                                                               \
+        if ((x - 0x01010101u) & ~x & 0x80808080u) { /* a 0x07 byte in this word */                              \
+            ZMTP_SIG(Q, 0)                                                                                       \
+            ZMTP_SIG(Q, 1)                                                                                       \
+            ZMTP_SIG(Q, 2)                                                                                       \
+            ZMTP_SIG(Q, 3)                                                                                       \
+        }                                                                                                        \
     }
-    __syncthreads();
-    const uint32_t nl = lcount < (uint32_t) kZmtpScanList ? lcount : (uint32_t) kZmtpScanList;
+        ZMTP_WORD(0)
+        ZMTP_WORD(1)
+        ZMTP_WORD(2)
+        ZMTP_WORD(3)
+#undef ZMTP_WORD
+#undef ZMTP_SIG
+        uint32_t total;
+        const uint32_t off = zmtp_block_excl(cnt, total);
+#pragma unroll
+        for (uint32_t c = 0; c < 2; ++c)
+            if (c < cnt)
+                dst0[base_out + off + c] = found[c];
+        base_out += total;
+    }
     if (threadIdx.x == 0)
-        gbase = nl ? atomicAdd(count, (unsigned long long) nl) : 0ull;
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x)
-        cand[gbase + k] = list[k];
+        count_wg[blockIdx.x] = base_out;
 }
 
-// candidate k's frame does not end at candidate k+1 (the last one never does)
-struct ZmtpIsUnlinked {
-    const uint8_t *b;
-    uint64_t n;
-    const uint64_t *cand;
-    const unsigned long long *m; // candidates
-    __device__ bool operator()(const uint64_t &k) const
-    {
-        if (k + 1 >= *m)
-            return true;
-        uint32_t hdr;
-        uint64_t size;
-        zmtp_header(b, n, cand[k], hdr, size);
-        return cand[k + 1] != cand[k] + hdr + size;
-    }
-};
+// Workgroup lists -> the sorted candidate array (off_wg: exclusive sum of the
+// counts, off_wg[nwg] = m).
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint64_t *cand_wg, const uint64_t *count_wg,
+                                                               const uint64_t *off_wg, uint64_t *cand)
+{
+    const uint32_t w = blockIdx.x, c = (uint32_t) count_wg[w];
+    const uint64_t o = off_wg[w];
+    for (uint32_t k = threadIdx.x; k < c; k += kZmtpThreads)
+        cand[o + k] = cand_wg[(size_t) w * kZmtpWgCap + k];
+}
 
-// Parse state written by k_zmtp_walk (device; read back by the host).
+// Links: candidate k is unlinked when its frame does not end at candidate
+// k+1 (the last one never does).  Over segments of 256 candidates (a
+// persistent grid; m is read on the device): nb[k] = the first unlinked index
+// >= k inside k's segment (or none), first_seg[s] = nb of segment s's first
+// candidate.
+constexpr uint32_t kZmtpSeg = 256;
+__global__ __launch_bounds__(kZmtpSeg) void k_zmtp_links(const uint8_t *b, uint64_t n, const uint64_t *cand,
+                                                         const uint64_t *m_p, uint64_t *nb, uint64_t *first_seg)
+{
+    __shared__ unsigned long long sh[kZmtpSeg / 64];
+    const uint64_t m = *m_p, nseg = (m + kZmtpSeg - 1) / kZmtpSeg;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint64_t sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const uint64_t k = sg * kZmtpSeg + threadIdx.x;
+        unsigned long long u = kZmtpNone;
+        if (k < m) {
+            bool unl = k + 1 >= m;
+            if (!unl) {
+                uint32_t hdr;
+                uint64_t size;
+                zmtp_header(b, n, cand[k], hdr, size);
+                unl = cand[k + 1] != cand[k] + hdr + size;
+            }
+            u = unl ? k : kZmtpNone;
+        }
+        // suffix minimum: within the wave, then over the later waves
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long o = __shfl_down(u, d);
+            if (lane + d < 64u && o < u)
+                u = o;
+        }
+        if (lane == 0)
+            sh[wv] = u;
+        __syncthreads();
+        for (uint32_t q = wv + 1; q < kZmtpSeg / 64; ++q)
+            if (sh[q] < u)
+                u = sh[q];
+        if (k < m)
+            nb[k] = u;
+        if (threadIdx.x == 0)
+            first_seg[sg] = u;
+        __syncthreads();
+    }
+}
+
+// first_seg -> its suffix minimum over segments, in place (one workgroup of
+// 1024 threads, each a contiguous run of segments): the first unlinked
+// candidate in segments >= s.
+constexpr uint32_t kZmtpNextThreads = 1024;
+__device__ void zmtp_segnext(uint64_t *first_seg, const uint64_t *m_p)
+{
+    __shared__ unsigned long long sh[kZmtpNextThreads];
+    const uint64_t nseg = (*m_p + kZmtpSeg - 1) / kZmtpSeg;
+    const uint64_t per = (nseg + kZmtpNextThreads - 1) / kZmtpNextThreads;
+    const uint64_t r0 = threadIdx.x * per, r1 = r0 + per < nseg ? r0 + per : nseg;
+    unsigned long long mn = kZmtpNone;
+    for (uint64_t s = r0; s < r1; ++s)
+        mn = first_seg[s] < mn ? first_seg[s] : mn;
+    sh[threadIdx.x] = mn;
+    __syncthreads();
+    for (uint32_t d = 1; d < kZmtpNextThreads; d <<= 1) {
+        const unsigned long long o = threadIdx.x + d < kZmtpNextThreads ? sh[threadIdx.x + d] : kZmtpNone;
+        __syncthreads();
+        if (o < sh[threadIdx.x])
+            sh[threadIdx.x] = o;
+        __syncthreads();
+    }
+    unsigned long long c = threadIdx.x + 1 < kZmtpNextThreads ? sh[threadIdx.x + 1] : kZmtpNone;
+    for (uint64_t s = r1; s-- > r0;) {
+        const unsigned long long x = first_seg[s];
+        c = x < c ? x : c;
+        first_seg[s] = c;
+    }
+}
+
+// Exclusive sum of v[0..n) into o[0..n] (o[n] = total) by one workgroup of
+// 1024 threads, each a contiguous run: the small scans of this path (the
+// workgroups' candidate counts; the frames' payload sizes) in one launch.
+constexpr uint32_t kZmtpScan1 = 1024;
+__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_exsum(const uint64_t *v, uint64_t n, uint64_t *o)
+{
+    __shared__ unsigned long long sh[kZmtpScan1];
+    const uint64_t per = (n + kZmtpScan1 - 1) / kZmtpScan1;
+    const uint64_t r0 = threadIdx.x * per, r1 = r0 + per < n ? r0 + per : n;
+    unsigned long long t = 0;
+    for (uint64_t i = r0; i < r1; ++i)
+        t += v[i];
+    sh[threadIdx.x] = t;
+    __syncthreads();
+    for (uint32_t d = 1; d < kZmtpScan1; d <<= 1) {
+        const unsigned long long x = threadIdx.x >= d ? sh[threadIdx.x - d] : 0ull;
+        __syncthreads();
+        sh[threadIdx.x] += x;
+        __syncthreads();
+    }
+    unsigned long long acc = sh[threadIdx.x] - t;
+    for (uint64_t i = r0; i < r1; ++i) {
+        const unsigned long long x = v[i];
+        o[i] = acc;
+        acc += x;
+    }
+    if (threadIdx.x == kZmtpScan1 - 1)
+        o[n] = sh[kZmtpScan1 - 1];
+}
+
+// Parse state written by k_zmtp_walk (device).
 struct ZmtpWalk {
     unsigned long long frames;   // frames returned (chain + an extra last one)
     unsigned long long consumed; // bytes of the buffer those frames cover
@@ -206,22 +388,26 @@ struct ZmtpWalk {
 };
 
 // Thread 0 walks the chain (see the file comment).  run[2r], run[2r+1]: the
-// first and last candidate of run r; runpre[r]: frames before run r.
-__global__ void k_zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_t max_frames, const uint64_t *cand,
-                            const unsigned long long *m_p, const uint64_t *bad, const unsigned long long *nbad_p,
-                            uint64_t *run, uint64_t *runpre, ZmtpWalk *out)
+// first and last candidate of run r; runpre[r]: frames before run r.  The
+// next unlinked candidate >= cur is nb[cur], or (none left in cur's
+// segment) first_seg[cur / kZmtpSeg + 1].
+__device__ void zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_t max_frames, const uint64_t *cand,
+                          const uint64_t *m_p, const uint64_t *nb, const uint64_t *first_seg, uint64_t *run,
+                          uint64_t *runpre, ZmtpWalk *out)
 {
-    if (blockIdx.x != 0 || threadIdx.x != 0)
-        return;
-    const uint64_t m = *m_p, nbad = *nbad_p;
-    uint64_t frames = 0, runs = 0, q = 0, bi = 0;
+    const uint64_t m = *m_p, nseg = (m + kZmtpSeg - 1) / kZmtpSeg;
+    uint64_t frames = 0, runs = 0, q = 0;
     bool full = false;
     if (m > 0 && cand[0] == 0 && max_frames > 0) {
         uint64_t cur = 0;
         for (;;) {
-            while (bi < nbad && bad[bi] < cur)
-                ++bi;
-            uint64_t last = bi < nbad ? bad[bi] : m - 1; // the run's last candidate
+            uint64_t last = nb[cur];
+            if (last == kZmtpNone) {
+                const uint64_t sg = cur / kZmtpSeg + 1u;
+                last = sg < nseg ? first_seg[sg] : kZmtpNone;
+            }
+            if (last == kZmtpNone)
+                last = m - 1; // (the last candidate is always unlinked)
             if (frames + (last - cur + 1) >= max_frames) {
                 last = cur + (max_frames - frames) - 1;
                 full = true;
@@ -275,64 +461,100 @@ __global__ void k_zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint6
     *out = w;
 }
 
-// Frame descriptors from the runs: one thread per candidate.
-__global__ void k_zmtp_frames(const uint8_t *b, uint64_t n, const uint64_t *cand, const unsigned long long *m_p,
-                              const uint64_t *run, const uint64_t *runpre, const ZmtpWalk *walk, uint64_t *f_off,
-                              uint32_t *f_len, uint8_t *f_flags)
+// first_seg's suffix minimum (k_zmtp_segnext), then thread 0 walks.
+__global__ __launch_bounds__(kZmtpNextThreads) void k_zmtp_next_walk(const uint8_t *b, uint64_t n, int64_t max_msg,
+                                                                     uint64_t max_frames, const uint64_t *cand,
+                                                                     const uint64_t *m_p, const uint64_t *nb,
+                                                                     uint64_t *first_seg, uint64_t *run,
+                                                                     uint64_t *runpre, ZmtpWalk *out)
 {
-    const uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t runs = walk->runs;
-    if (k == 0 && walk->extra) {
+    zmtp_segnext(first_seg, m_p);
+    __threadfence_block();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        zmtp_walk(b, n, max_msg, max_frames, cand, m_p, nb, first_seg, run, runpre, out);
+}
+
+// Frame descriptors from the runs: one workgroup per candidate segment
+// (k_zmtp_links's layout).  Entries [frames, max_frames) get an empty frame
+// (offset 0, length 0: the decode reports it malformed and writes nothing
+// else), so the decode can run over max_frames without the frame count
+// reaching the host.
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, uint64_t n, const uint64_t *cand,
+                                                              const uint64_t *m_p, const uint64_t *run,
+                                                              const uint64_t *runpre, const ZmtpWalk *walk,
+                                                              uint64_t max_frames, uint64_t *f_off, uint32_t *f_len,
+                                                              uint8_t *f_flags, uint32_t *sid_fill, uint32_t sid,
+                                                              uint64_t *psize)
+{
+    const uint64_t runs = walk->runs, frames = walk->frames, m = *m_p;
+    const uint64_t stride = (uint64_t) gridDim.x * kZmtpThreads;
+    // padding and the per-frame session over max_frames
+    for (uint64_t j = (uint64_t) blockIdx.x * kZmtpThreads + threadIdx.x; j < max_frames; j += stride) {
+        sid_fill[j] = sid;
+        if (j >= frames) {
+            f_off[j] = 0;
+            f_len[j] = 0;
+            f_flags[j] = 0;
+            psize[j] = 0;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        psize[max_frames] = 0; // the scan's last entry is the total
+    if (blockIdx.x == 0 && threadIdx.x == 0 && walk->extra) {
         uint32_t hdr;
         uint64_t size;
         const uint64_t q = walk->extra_off;
         zmtp_header(b, n, q, hdr, size);
-        const uint64_t j = walk->frames - 1;
+        const uint64_t j = frames - 1;
         f_off[j] = q + hdr;
         f_len[j] = (uint32_t) size;
         f_flags[j] = b[q];
+        psize[j] = size >= 33u ? size - 33u : 0u;
     }
-    if (k >= *m_p || runs == 0)
+    if (runs == 0)
         return;
-    // the run holding k: last run whose first candidate <= k
-    uint64_t lo = 0, hi = runs;
-    while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (run[2 * mid] <= k)
-            lo = mid;
-        else
-            hi = mid;
+    for (uint64_t k = (uint64_t) blockIdx.x * kZmtpThreads + threadIdx.x; k < m; k += stride) {
+        // the run holding k: last run whose first candidate <= k
+        uint64_t lo = 0, hi = runs;
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (run[2 * mid] <= k)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        if (k < run[2 * lo] || k > run[2 * lo + 1])
+            continue; // not on the chain
+        const uint64_t j = runpre[lo] + (k - run[2 * lo]);
+        uint32_t hdr;
+        uint64_t size;
+        zmtp_header(b, n, cand[k], hdr, size);
+        f_off[j] = cand[k] + hdr;
+        f_len[j] = (uint32_t) size;
+        f_flags[j] = b[cand[k]];
+        psize[j] = size >= 33u ? size - 33u : 0u; // payload bytes (the offsets scan)
     }
-    if (k < run[2 * lo] || k > run[2 * lo + 1])
-        return; // not on the chain
-    const uint64_t j = runpre[lo] + (k - run[2 * lo]);
-    uint32_t hdr;
-    uint64_t size;
-    zmtp_header(b, n, cand[k], hdr, size);
-    f_off[j] = cand[k] + hdr;
-    f_len[j] = (uint32_t) size;
-    f_flags[j] = b[cand[k]];
-}
-
-// Payload bytes per frame (the decode output), for the offsets scan.
-__global__ void k_zmtp_payload_sizes(uint64_t nf, const uint32_t *f_len, uint64_t *psize, uint32_t *sid_fill,
-                                     uint32_t sid)
-{
-    const uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (j > nf)
-        return;
-    psize[j] = j < nf && f_len[j] >= 33u ? f_len[j] - 33u : 0u;
-    if (j < nf)
-        sid_fill[j] = sid;
 }
 
 // msg_t flags of a decoded frame: the ZMTP frame's MORE / COMMAND bits
 // (src/v2_decoder.cpp:35-41) ORed with the plaintext's (set_flags ORs,
 // src/msg.cpp:433-436); 0 for a frame that failed.
-__global__ void k_zmtp_flags(uint64_t nf, const uint8_t *f_flags, const int32_t *status, uint8_t *flags_out)
+// (and, thread 0, the call's result: frames, bytes consumed, payload
+// bytes, error -- one read back, or none for the asynchronous form)
+__global__ void k_zmtp_flags(const ZmtpWalk *walk, uint64_t max_frames, const uint8_t *f_flags, const int32_t *status,
+                             uint8_t *flags_out, const uint64_t *poff, zmqg_zmtp_result *res)
 {
     const uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nf || status[j] != 0)
+    if (j == 0) {
+        zmqg_zmtp_result r{};
+        r.frames = walk->frames;
+        r.consumed = walk->consumed;
+        r.error = walk->error;
+        r.out_bytes = poff[walk->frames];
+        *res = r;
+    }
+    if (j >= max_frames || j >= walk->frames || status[j] != 0)
         return;
     const uint8_t z = f_flags[j];
     flags_out[j] |= (uint8_t) (((z & kZmtpMore) ? 1u : 0u) | ((z & kZmtpCommand) ? 2u : 0u));

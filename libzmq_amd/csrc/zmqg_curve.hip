@@ -160,19 +160,23 @@ struct ZmtpWs {
     uint64_t n_cap = 0;                   // send side: frames
     uint64_t *F = nullptr;                // [n_cap + 1] frame bytes
     uint64_t *wire_off = nullptr;         // [n_cap] body offsets
+    uint64_t g_cap = 0;                   // receive side: 16 KiB workgroups of the stream
     uint64_t c_cap = 0;                   // receive side: candidates
-    uint64_t f_cap = 0;                   // receive side: frames
-    uint64_t *cand = nullptr;             // [c_cap]
-    uint64_t *bad = nullptr;              // [c_cap]
-    uint64_t *cand0 = nullptr;            // [c_cap] candidates as found (unordered)
-    uint64_t *run = nullptr;              // [2 c_cap]
-    uint64_t *runpre = nullptr;           // [c_cap]
-    uint64_t *psize = nullptr;            // [c_cap + 1]
-    uint64_t *poff = nullptr;             // [c_cap + 1]
-    uint32_t *sid_fill = nullptr;         // [c_cap]
-    uint8_t *fflags = nullptr;            // [c_cap]
-    unsigned long long *counts = nullptr; // [2] candidates, unlinked candidates
+    uint64_t f_cap = 0;                   // receive side: frames (max_frames)
+    uint64_t *cand_wg = nullptr;          // [g_cap * kZmtpWgCap] each workgroup's candidates, in order
+    uint64_t *count_wg = nullptr;         // [g_cap + 1]
+    uint64_t *off_wg = nullptr;           // [g_cap + 1] exclusive sum of count_wg
+    uint64_t *cand = nullptr;             // [c_cap] sorted candidates
+    uint64_t *nb = nullptr;               // [c_cap] next unlinked candidate in the 256-candidate segment
+    uint64_t *first_seg = nullptr;        // [c_cap / 256 + 1] first unlinked candidate in segments >= s
+    uint64_t *run = nullptr;              // [2 (f_cap + 1)]
+    uint64_t *runpre = nullptr;           // [f_cap + 1]
+    uint64_t *psize = nullptr;            // [f_cap + 1]
+    uint64_t *poff = nullptr;             // [f_cap + 1]
+    uint32_t *sid_fill = nullptr;         // [f_cap]
+    uint8_t *fflags = nullptr;            // [f_cap]
     ZmtpWalk *walk = nullptr;
+    zmqg_zmtp_result *res = nullptr;      // the synchronous call's result on the device
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };
@@ -2003,8 +2007,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
             (void) hipFree(p);
     {
         ZmtpWs &z = ctx->zw;
-        void *zp[] = {z.F, z.wire_off, z.cand, z.bad, z.cand0, z.run, z.runpre, z.psize, z.poff, z.sid_fill, z.fflags,
-                      z.counts, z.walk, z.temp};
+        void *zp[] = {z.F,      z.wire_off, z.cand_wg, z.count_wg, z.off_wg,   z.cand,   z.nb,   z.first_seg, z.run,
+                      z.runpre, z.psize,    z.poff,    z.sid_fill, z.fflags,   z.walk,   z.res,  z.temp};
         for (void *p : zp)
             if (p)
                 (void) hipFree(p);
@@ -2520,116 +2524,143 @@ int zmqg_encode_zmtp(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     return zmqg_encode_batch(ctx, n, sid, nonce, flags, in_off, len, in, z.wire_off, out, stream);
 }
 
-int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
-                     uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
-                     uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result, void *stream)
+int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
+                           uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
+                           uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result,
+                           void *stream)
 {
     if (!ctx || !result || sid >= ctx->max_sessions || in_bytes > 0x7fffffffull || check_n(max_frames))
         return -EINVAL;
-    memset(result, 0, sizeof *result);
-    if (in_bytes == 0 || max_frames == 0)
+    hipStream_t st = (hipStream_t) stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    if (in_bytes == 0 || max_frames == 0) {
+        ZCHECK(ctx, hipMemsetAsync(result, 0, sizeof *result, st));
         return 0;
+    }
     if (!in || !frame_in_off || !frame_len || !out_off || !out || !flags_out || !status_out)
         return -EINVAL;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    hipStream_t st = (hipStream_t) stream;
-    ZCHECK(ctx, hipSetDevice(ctx->device));
     ZmtpWs &z = ctx->zw;
     int rc;
-    // candidates: at most two per "\x07MESSAGE" occurrence, occurrences >= 8 bytes apart
-    const uint64_t ccap = in_bytes / 4 + 2;
+    const uint64_t nwg = (in_bytes + kZmtpWgBytes - 1) / kZmtpWgBytes;
+    if (nwg > z.g_cap) {
+        uint64_t cap = z.g_cap ? z.g_cap : 64;
+        while (cap < nwg)
+            cap *= 2;
+        if ((rc = grow(ctx, z.cand_wg, cap * kZmtpWgCap, st)) || (rc = grow(ctx, z.count_wg, cap + 1, st)) ||
+            (rc = grow(ctx, z.off_wg, cap + 1, st)))
+            return rc;
+        z.g_cap = cap;
+    }
+    // candidates: signatures are >= 8 bytes apart, one candidate each
+    const uint64_t ccap = in_bytes / 8 + 2;
     if (ccap > z.c_cap) {
         uint64_t cap = z.c_cap ? z.c_cap : 1024;
         while (cap < ccap)
             cap *= 2;
-        if ((rc = grow(ctx, z.cand, cap, st)) || (rc = grow(ctx, z.bad, cap, st)) || (rc = grow(ctx, z.cand0, cap, st)))
+        if ((rc = grow(ctx, z.cand, cap, st)) || (rc = grow(ctx, z.nb, cap, st)) ||
+            (rc = grow(ctx, z.first_seg, cap / kZmtpSeg + 2, st)))
             return rc;
         z.c_cap = cap;
     }
-    // frames (and chain runs, each holding a frame): at most max_frames
-    const uint64_t fcap = max_frames < ccap ? max_frames : ccap;
-    if (fcap > z.f_cap) {
+    if (max_frames > z.f_cap) {
         uint64_t cap = z.f_cap ? z.f_cap : 1024;
-        while (cap < fcap)
+        while (cap < max_frames)
             cap *= 2;
-        if ((rc = grow(ctx, z.run, 2 * cap, st)) || (rc = grow(ctx, z.runpre, cap, st)) || (rc = grow(ctx, z.psize, cap + 1, st)) ||
-            (rc = grow(ctx, z.poff, cap + 1, st)) || (rc = grow(ctx, z.sid_fill, cap, st)) || (rc = grow(ctx, z.fflags, cap, st)))
+        if ((rc = grow(ctx, z.run, 2 * (cap + 1), st)) || (rc = grow(ctx, z.runpre, cap + 1, st)) ||
+            (rc = grow(ctx, z.psize, cap + 1, st)) || (rc = grow(ctx, z.poff, cap + 1, st)) ||
+            (rc = grow(ctx, z.sid_fill, cap, st)) || (rc = grow(ctx, z.fflags, cap, st)))
             return rc;
         z.f_cap = cap;
     }
-    if (!z.counts && (rc = grow(ctx, z.counts, 3, st)))
-        return rc;
     if (!z.walk && (rc = grow(ctx, z.walk, 1, st)))
         return rc;
-    hipcub::CountingInputIterator<uint64_t> pos(0);
-    // candidates (unordered), then sorted by offset
-    ZCHECK(ctx, hipMemsetAsync(z.counts, 0, 3 * sizeof(unsigned long long), st));
-    const uint64_t per_wg = 256ull * 16u * kZmtpScanIters;
-    hipLaunchKernelGGL(k_zmtp_scan, dim3((unsigned) ((in_bytes + per_wg - 1) / per_wg)), dim3(256), 0, st, in,
-                       in_bytes, max_msg_size, z.cand0, z.counts);
+    const uint32_t g = (uint32_t) nwg;
+    // persistent grids over device-side counts: enough workgroups to cover
+    // config-2-sized streams in one pass
+    const uint32_t pg = (uint32_t) (ctx->cus > 0 ? 4 * ctx->cus : 1024);
+    const uint64_t *m_p = z.off_wg + nwg; // the candidate count, on the device
+    // 1. candidates, in stream order
+    hipLaunchKernelGGL(k_zmtp_scan, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
+                       z.count_wg);
     ZCHECK(ctx, hipGetLastError());
-    unsigned long long m = 0;
-    ZCHECK(ctx, hipMemcpyAsync(&m, z.counts, sizeof m, hipMemcpyDeviceToHost, st));
-    ZCHECK(ctx, hipStreamSynchronize(st));
-    size_t need = 0, tb = 0;
-    if (m > 0) {
-        int bits = 1;
-        while (bits < 64 && (1ull << bits) < in_bytes)
-            ++bits;
-        ZCHECK(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, need, z.cand0, z.cand, (int) m, 0, bits, st));
-        if ((rc = zmtp_temp(ctx, need, st)))
+    // the workgroup counts: one workgroup scans up to 8 per thread; the
+    // payload sizes (max_frames + 1 entries) always go to hipCUB
+    const bool small_scan = nwg <= 8u * kZmtpScan1;
+    size_t tb;
+    {
+        size_t need = 0, need2 = 0;
+        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.count_wg, z.off_wg, (int) (nwg + 1), st));
+        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need2, z.psize, z.poff, (int) (max_frames + 1), st));
+        if ((rc = zmtp_temp(ctx, need > need2 ? need : need2, st)))
             return rc;
-        tb = z.temp_bytes;
-        ZCHECK(ctx, hipcub::DeviceRadixSort::SortKeys(z.temp, tb, z.cand0, z.cand, (int) m, 0, bits, st));
     }
-    if (m > 0) {
-        const ZmtpIsUnlinked isu{in, in_bytes, z.cand, z.counts};
-        need = 0;
-        ZCHECK(ctx, hipcub::DeviceSelect::If(nullptr, need, pos, z.bad, z.counts + 1, (int) m, isu, st));
-        if ((rc = zmtp_temp(ctx, need, st)))
-            return rc;
-        tb = z.temp_bytes;
-        ZCHECK(ctx, hipcub::DeviceSelect::If(z.temp, tb, pos, z.bad, z.counts + 1, (int) m, isu, st));
+    if (small_scan) {
+        hipLaunchKernelGGL(k_zmtp_exsum, dim3(1), dim3(kZmtpScan1), 0, st, (const uint64_t *) z.count_wg, nwg,
+                           z.off_wg);
+        ZCHECK(ctx, hipGetLastError());
     } else {
-        ZCHECK(ctx, hipMemsetAsync(z.counts + 1, 0, sizeof(unsigned long long), st));
+        ZCHECK(ctx, hipMemsetAsync(z.count_wg + nwg, 0, sizeof(uint64_t), st));
+        tb = z.temp_bytes;
+        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.count_wg, z.off_wg, (int) (nwg + 1), st));
     }
-    hipLaunchKernelGGL(k_zmtp_walk, dim3(1), dim3(64), 0, st, in, in_bytes, max_msg_size, max_frames, z.cand,
-                       z.counts, z.bad, z.counts + 1, z.run, z.runpre, z.walk);
+    hipLaunchKernelGGL(k_zmtp_compact, dim3(g), dim3(kZmtpThreads), 0, st, (const uint64_t *) z.cand_wg,
+                       (const uint64_t *) z.count_wg, (const uint64_t *) z.off_wg, z.cand);
     ZCHECK(ctx, hipGetLastError());
-    const uint64_t mt = m ? m : 1;
-    hipLaunchKernelGGL(k_zmtp_frames, dim3((unsigned) ((mt + 255) / 256)), dim3(256), 0, st, in, in_bytes, z.cand,
-                       z.counts, z.run, z.runpre, z.walk, frame_in_off, frame_len, z.fflags);
+    // 2. links
+    hipLaunchKernelGGL(k_zmtp_links, dim3(pg), dim3(kZmtpSeg), 0, st, in, in_bytes, (const uint64_t *) z.cand, m_p,
+                       z.nb, z.first_seg);
     ZCHECK(ctx, hipGetLastError());
-    ZmtpWalk w;
-    ZCHECK(ctx, hipMemcpyAsync(&w, z.walk, sizeof w, hipMemcpyDeviceToHost, st));
-    ZCHECK(ctx, hipStreamSynchronize(st));
-    result->frames = w.frames;
-    result->consumed = w.consumed;
-    result->error = w.error;
-    const uint64_t nf = w.frames;
-    if (nf == 0)
-        return 0;
-    hipLaunchKernelGGL(k_zmtp_payload_sizes, dim3((unsigned) ((nf + 1 + 255) / 256)), dim3(256), 0, st, nf,
-                       frame_len, z.psize, z.sid_fill, sid);
+    // 3. the next unlinked candidate per segment, then the walk (one launch)
+    hipLaunchKernelGGL(k_zmtp_next_walk, dim3(1), dim3(kZmtpNextThreads), 0, st, in, in_bytes, max_msg_size,
+                       max_frames, (const uint64_t *) z.cand, m_p, (const uint64_t *) z.nb, z.first_seg, z.run,
+                       z.runpre, z.walk);
     ZCHECK(ctx, hipGetLastError());
-    need = 0;
-    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.psize, z.poff, (int) (nf + 1), st));
-    if ((rc = zmtp_temp(ctx, need, st)))
-        return rc;
+    // 4. descriptors (empty frames up to max_frames), payload offsets
+    hipLaunchKernelGGL(k_zmtp_frames, dim3(pg), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand, m_p,
+                       (const uint64_t *) z.run, (const uint64_t *) z.runpre, (const ZmtpWalk *) z.walk, max_frames,
+                       frame_in_off, frame_len, z.fflags, z.sid_fill, sid, z.psize);
+    ZCHECK(ctx, hipGetLastError());
     tb = z.temp_bytes;
-    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.psize, z.poff, (int) (nf + 1), st));
-    ZCHECK(ctx, hipMemcpyAsync(out_off, z.poff, nf * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
-    rc = zmqg_decode_batch(ctx, nf, z.sid_fill, frame_in_off, frame_len, in, z.poff, out, flags_out, status_out,
-                           stream);
+    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.psize, z.poff, (int) (max_frames + 1), st));
+    ZCHECK(ctx, hipMemcpyAsync(out_off, z.poff, max_frames * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    // the decode over max_frames (the empty frames fail as malformed and
+    // write nothing else); a maxmsgsize within the frame kernel's range bounds
+    // every frame, so the large-frame launches are skipped
+    zmqg_batch_opts o{};
+    o.size = sizeof o;
+    if (max_msg_size >= 0 && (uint64_t) max_msg_size <= kMaxFrameStream)
+        o.max_len = max_msg_size > 0 ? (uint64_t) max_msg_size : 1u;
+    rc = zmqg_decode_batch_ex(ctx, max_frames, z.sid_fill, frame_in_off, frame_len, in, z.poff, out, flags_out,
+                              status_out, o.max_len ? &o : nullptr, stream);
     if (rc)
         return rc;
-    hipLaunchKernelGGL(k_zmtp_flags, dim3((unsigned) ((nf + 255) / 256)), dim3(256), 0, st, nf, z.fflags,
-                       status_out, flags_out);
+    hipLaunchKernelGGL(k_zmtp_flags, dim3((unsigned) ((max_frames + 255) / 256)), dim3(256), 0, st,
+                       (const ZmtpWalk *) z.walk, max_frames, (const uint8_t *) z.fflags, (const int32_t *) status_out,
+                       flags_out, (const uint64_t *) z.poff, result);
     ZCHECK(ctx, hipGetLastError());
-    unsigned long long ob = 0;
-    ZCHECK(ctx, hipMemcpyAsync(&ob, z.poff + nf, sizeof ob, hipMemcpyDeviceToHost, st));
+    return 0;
+}
+
+int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
+                     uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
+                     uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result, void *stream)
+{
+    if (!ctx || !result)
+        return -EINVAL;
+    memset(result, 0, sizeof *result);
+    hipStream_t st = (hipStream_t) stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    if (!ctx->zw.res && (rc = grow(ctx, ctx->zw.res, 1, st)))
+        return rc;
+    rc = zmqg_decode_zmtp_async(ctx, sid, in, in_bytes, max_msg_size, max_frames, frame_in_off, frame_len, out_off,
+                                out, flags_out, status_out, ctx->zw.res, stream);
+    if (rc)
+        return rc;
+    // the one read back of the call
+    ZCHECK(ctx, hipMemcpyAsync(result, ctx->zw.res, sizeof *result, hipMemcpyDeviceToHost, st));
     ZCHECK(ctx, hipStreamSynchronize(st));
-    result->out_bytes = ob;
     return 0;
 }
 

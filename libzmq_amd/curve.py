@@ -83,6 +83,7 @@ class ZmtpResult(ctypes.Structure):  # zmqg_zmtp_result
 _lib.zmqg_encode_zmtp.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_zmtp.argtypes = [_P, _U32, _P, _U64, ctypes.c_int64, _U64] + [_P] * 6 + [ctypes.POINTER(ZmtpResult),
                                                                                        _P]
+_lib.zmqg_decode_zmtp_async.argtypes = [_P, _U32, _P, _U64, ctypes.c_int64, _U64] + [_P] * 8
 _lib.zmqg_scalarmult_batch.argtypes = [_P, _U64] + [_P] * 5
 _lib.zmqg_box_beforenm_batch.argtypes = [_P, _U64] + [_P] * 5
 _lib.zmqg_box_afternm_batch.argtypes = [_P, _U64] + [_P] * 8
@@ -258,6 +259,22 @@ class CurveContext:
                                           _ptr(flags_out), _ptr(status_out), ctypes.byref(r),
                                           _stream_handle(stream)), "zmqg_decode_zmtp")
         return dict(frames=r.frames, consumed=r.consumed, out_bytes=r.out_bytes, error=r.error)
+
+    def decode_zmtp_async(self, sid, inp, in_bytes, max_msg_size, max_frames, frame_in_off, frame_len, out_off, out,
+                          flags_out, status_out, result, stream=None):
+        """The same without synchronising: `result` is a device int64 tensor of
+        4 entries (zmqg_zmtp_result: frames, consumed, out_bytes, error | pad)
+        filled when the stream gets there; read it with zmtp_result()."""
+        self._check(_lib.zmqg_decode_zmtp_async(self._ctx, sid, _ptr(inp), in_bytes, max_msg_size, max_frames,
+                                                _ptr(frame_in_off), _ptr(frame_len), _ptr(out_off), _ptr(out),
+                                                _ptr(flags_out), _ptr(status_out), _ptr(result),
+                                                _stream_handle(stream)), "zmqg_decode_zmtp_async")
+
+    @staticmethod
+    def zmtp_result(result):
+        r = result.cpu().numpy().view(np.uint64)
+        return dict(frames=int(r[0]), consumed=int(r[1]), out_bytes=int(r[2]),
+                    error=int(np.int32(r[3] & np.uint64(0xffffffff))))
 
     # ---- handshake key derivation (device tensors of n x 32 bytes) ----
     def scalarmult_batch(self, scalar, point, out, status_out, stream=None):

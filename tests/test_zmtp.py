@@ -80,13 +80,17 @@ def _stream_case(rng, case, precom, n=400):
     wire = O.encode_batch(sessions, b["sid"], b["nonce"], b["flags"], b["in_off"], b["lens"], b["inp"], out_off, wtotal)
     bodies = [bytearray(wire[int(out_off[i]):int(out_off[i]) + int(wl[i])].tobytes()) for i in range(n)]
     frames = []
-    max_msg, max_frames = -1, 1 << 20
+    max_msg, max_frames = -1, 1000  # the arrays below hold max_frames entries (include/zmqg_curve.h)
     for i, body in enumerate(bodies):
         if case == "planted" and rng.random() < 0.2 and len(body) > 60:
             # a frame-like header and the MESSAGE signature inside the ciphertext
             k = int(rng.integers(33, len(body) - 20))
             fake = bytes([0, int(rng.integers(8, 40))]) + b"\x07MESSAGE"
             body[k:k + len(fake)] = fake
+        if case == "flood" and rng.random() < 0.3 and len(body) > 100:
+            # a frame-like header + signature every 16 bytes of the ciphertext
+            pat = (b"\x00\x10\x07MESSAGE" + bytes(6)) * ((len(body) - 49) // 16)
+            body[33:33 + len(pat)] = pat
         if case == "large_small" and rng.random() < 0.3 and len(body) <= 255:
             frames.append(bytes([Z.LARGE]) + struct.pack(">Q", len(body)) + bytes(body))
             continue
@@ -113,15 +117,15 @@ def _stream_case(rng, case, precom, n=400):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["clean", "truncated", "planted", "large_small", "ping", "emsgsize", "max_frames",
-                                  "zmtp_flags"])
+@pytest.mark.parametrize("case", ["clean", "truncated", "planted", "flood", "large_small", "ping", "emsgsize",
+                                  "max_frames", "zmtp_flags"])
 def test_decode_zmtp_matches_oracle(torch_cuda, C, case):
     torch = torch_cuda
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     stream, max_msg, max_frames = _stream_case(rng, case, precom)
-    ref = Z.parse(stream, max_msg, max_frames if max_frames < (1 << 20) else None)
+    ref = Z.parse(stream, max_msg, max_frames)
     # CURVE decode of the frames the decoder produced, in order (peer nonce 2)
     fr = ref["frames"]
     nf = len(fr)
@@ -145,7 +149,14 @@ def test_decode_zmtp_matches_oracle(torch_cuda, C, case):
     d_out = torch.full((len(stream) + 1,), 0x77, dtype=torch.uint8, device=dev)
     d_fl = torch.zeros(cap, dtype=torch.uint8, device=dev)
     d_st = torch.full((cap,), -1, dtype=torch.int32, device=dev)
-    r = ctx.decode_zmtp(0, d_in, len(stream), max_msg, max_frames, d_foff, d_flen, d_poff, d_out, d_fl, d_st)
+    if case == "clean":  # the asynchronous form, result read once the stream is done
+        res = torch.zeros(4, dtype=torch.int64, device=dev)
+        ctx.decode_zmtp_async(0, d_in, len(stream), max_msg, max_frames, d_foff, d_flen, d_poff, d_out, d_fl, d_st,
+                              res)
+        torch.cuda.synchronize()
+        r = ctx.zmtp_result(res)
+    else:
+        r = ctx.decode_zmtp(0, d_in, len(stream), max_msg, max_frames, d_foff, d_flen, d_poff, d_out, d_fl, d_st)
     assert r["frames"] == nf and r["consumed"] == ref["consumed"] and r["error"] == ref["error"], (r, ref["consumed"])
     assert r["out_bytes"] == int(plen.sum())
     assert (d_foff[:nf].cpu().numpy().view(np.uint64) == f_off).all()
@@ -168,7 +179,7 @@ def test_decode_zmtp_matches_oracle(torch_cuda, C, case):
     assert d_out[:int(plen.sum())].cpu().numpy().tobytes() == pl[:int(plen.sum())].tobytes()
     if case in ("clean", "large_small", "zmtp_flags"):
         assert (st == 0).all() and ref["consumed"] == len(stream)
-    if case == "planted":
+    if case in ("planted", "flood"):
         assert (st == C.ERR_CRYPTOGRAPHIC).any() and ref["consumed"] == len(stream)
     if case == "ping":
         assert st[-1] != 0 and (st[:-1] == 0).all()
