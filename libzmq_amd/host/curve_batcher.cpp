@@ -192,20 +192,22 @@ int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
         errno = EIO;
         return -1;
     }
-    const size_t plen = size_ >= 33 ? size_ - 33 : 0;
-    if (open_slot (decode_kind, size_, plen) != 0)
+    //  decoded in place: the payload is left where crypto_box_open_easy_afternm
+    //  leaves it in the reference, at wire offset 33 of the frame
+    //  (src/curve_mechanism_base.cpp:222-228), so a decode slot needs no
+    //  output area
+    if (open_slot (decode_kind, size_, 0) != 0)
         return -1;
     slot_t *s = _open[decode_kind];
     const size_t i = s->n++;
     s->sid[i] = conn_->_sid;
     s->in_off[i] = s->in_used;
     s->len[i] = static_cast<uint32_t> (size_);
-    s->out_off[i] = s->out_used;
+    s->out_off[i] = s->in_used + 33;
     s->tags[i] = tag_;
     if (size_)
         memcpy (s->in + s->in_used, wire_, size_);
     s->in_used += size_;
-    s->out_used += plen;
     return 0;
 }
 
@@ -218,7 +220,7 @@ int curve_batcher_t::launch (slot_t *s)
                                 _stream);
     else
         rc = zmqg_decode_batch (_ctx, s->n, s->sid, s->in_off, s->len, s->in,
-                                s->out_off, s->out, s->flags_out, s->status,
+                                s->out_off, s->in, s->flags_out, s->status,
                                 _stream);
     if (rc == 0)
         rc = zmqg_fence_record (_ctx, _stream, &s->fence);
@@ -244,7 +246,7 @@ int curve_batcher_t::deliver (slot_t *s)
     } else {
         for (size_t i = 0; i < s->n; ++i) {
             if (s->status[i] == 0)
-                _sink->on_decoded (s->tags[i], 0, s->out + s->out_off[i],
+                _sink->on_decoded (s->tags[i], 0, s->in + s->out_off[i],
                                    s->len[i] - 33u, s->flags_out[i]);
             else
                 _sink->on_decoded (s->tags[i], s->status[i], NULL, 0, 0);

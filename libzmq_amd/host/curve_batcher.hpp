@@ -24,7 +24,10 @@
 // Slots are page-locked, device-mapped host memory (zmqg_host_alloc): the
 // kernels read the payload and write the result over PCIe in place, so the
 // only host copies are the submit copy (the engine's own copy into its send
-// or receive buffer in the reference) and whatever the sink does.  Slots
+// or receive buffer in the reference) and whatever the sink does.  Decode
+// runs in place inside the slot's input area: each payload is left at wire
+// offset 33 of its frame, where the reference's crypto_box_open_easy_afternm
+// leaves it (src/curve_mechanism_base.cpp:222-228).  Slots
 // cycle free -> open -> in flight -> free; when none is free, a submit
 // blocks on the oldest in-flight slot and delivers it (back-pressure).
 //

@@ -2,10 +2,69 @@
 #include "curve_encoding_gpu.hpp"
 
 #include <errno.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <vector>
 
 namespace zmqg
 {
+namespace
+{
+struct thread_state_t
+{
+    zmqg_ctx *ctx;
+    bool failed;
+    uint32_t next;
+    std::vector<uint32_t> free_sids;
+    thread_state_t () : ctx (NULL), failed (false), next (0) {}
+    ~thread_state_t ()
+    {
+        if (ctx)
+            zmqg_ctx_destroy (ctx);
+    }
+};
+thread_local thread_state_t tls_state;
+}
+
+zmqg_ctx *thread_ctx ()
+{
+    thread_state_t &t = tls_state;
+    if (!t.ctx && !t.failed) {
+        const char *d = getenv ("ZMQG_DEVICE");
+        if (zmqg_ctx_create (d ? atoi (d) : 0, thread_sessions, &t.ctx) != 0) {
+            t.ctx = NULL;
+            t.failed = true;
+        }
+    }
+    return t.ctx;
+}
+
+int acquire_session (uint32_t *sid_)
+{
+    thread_state_t &t = tls_state;
+    if (!thread_ctx ()) {
+        errno = EIO;
+        return -1;
+    }
+    if (!t.free_sids.empty ()) {
+        *sid_ = t.free_sids.back ();
+        t.free_sids.pop_back ();
+        return 0;
+    }
+    if (t.next == thread_sessions) {
+        errno = ENOMEM;
+        return -1;
+    }
+    *sid_ = t.next++;
+    return 0;
+}
+
+void release_session (uint32_t sid_)
+{
+    tls_state.free_sids.push_back (sid_);
+}
+
 curve_encoding_gpu_t::curve_encoding_gpu_t (zmqg_ctx *ctx_,
                                             uint32_t sid_,
                                             const char *encode_nonce_prefix_,

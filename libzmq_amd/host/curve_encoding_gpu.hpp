@@ -47,6 +47,22 @@ struct msg_buf_t
     size_t size () const { return bytes.size (); }
 };
 
+//  Per-I/O-thread device context and session slots for the drop-in
+//  zmq::curve_encoding_t (zmq_curve_encoding.hpp).  libzmq runs each engine,
+//  and so each curve_encoding_t, on one I/O thread for its whole life
+//  (src/io_thread.hpp); a zmqg_ctx is externally synchronised, so each I/O
+//  thread gets its own, created on first use on device ZMQG_DEVICE (default
+//  0) with thread_sessions slots.  acquire_session returns 0 and a free slot
+//  of the calling thread's ctx, or -1 (errno ENOMEM: all slots in use, or EIO:
+//  the ctx could not be created); release_session returns the slot.
+enum
+{
+    thread_sessions = 4096
+};
+zmqg_ctx *thread_ctx ();
+int acquire_session (uint32_t *sid_);
+void release_session (uint32_t sid_);
+
 class curve_encoding_gpu_t
 {
   public:

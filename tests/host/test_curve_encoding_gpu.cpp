@@ -173,6 +173,30 @@ int main ()
         ++tests_run;
     }
     CHECK (zmqg_ctx_destroy (ctx) == 0);
+    {
+        //  per-I/O-thread ctx and session slots of the drop-in
+        //  zmq::curve_encoding_t (zmq_curve_encoding.hpp): a round trip
+        //  between two codecs on slots of the thread's ctx, and slot reuse
+        zmqg_ctx *tc = zmqg::thread_ctx ();
+        CHECK (tc != NULL && zmqg::thread_ctx () == tc);
+        uint32_t a = 99, b = 99, c = 99;
+        CHECK (zmqg::acquire_session (&a) == 0 && zmqg::acquire_session (&b) == 0 && a != b);
+        zmqg::curve_encoding_gpu_t cli (tc, a, client_prefix, server_prefix, false);
+        zmqg::curve_encoding_gpu_t srv (tc, b, server_prefix, client_prefix, false);
+        fill_precom (cli.get_writable_precom_buffer (), 5);
+        fill_precom (srv.get_writable_precom_buffer (), 5);
+        zmqg::msg_buf_t m;
+        m.bytes.assign (300, 0x5a);
+        CHECK (cli.encode (&m) == 0);
+        srv.set_peer_nonce (0); // (the handshake leaves it below the first MESSAGE nonce)
+        int ev = 0;
+        CHECK (srv.decode (&m, &ev) == 0 && m.bytes == std::vector<uint8_t> (300, 0x5a));
+        zmqg::release_session (a);
+        CHECK (zmqg::acquire_session (&c) == 0 && c == a);
+        zmqg::release_session (b);
+        zmqg::release_session (c);
+        ++tests_run;
+    }
     printf ("OK %d\n", tests_run);
     return 0;
 }

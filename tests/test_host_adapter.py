@@ -32,7 +32,7 @@ def test_adapter_roundtrips_on_gpu(tmp_path):
     exe = build_adapter_test(str(tmp_path))
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr + r.stdout
-    assert r.stdout.strip() == "OK 7"
+    assert r.stdout.strip() == "OK 8"
 
 
 def build_batcher_test(out_dir):
