@@ -271,12 +271,17 @@ int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
  * and curve_mechanism_base_t::decode over a received byte stream of one
  * connection (session sid), on the device.  Frames are found from offset 0;
  * up to max_frames of them are decoded: frame i's body is
- * in[frame_in_off[i] .. +frame_len[i]), its payload is written at
- * out[out_off[i]] and flags_out / status_out are as for zmqg_decode_batch,
+ * in[frame_in_off[i] .. +frame_len[i]), its payload (frame_len[i] - 33
+ * bytes) is written at out[out_off[i]] with out_off[i] = frame_in_off[i] --
+ * the body's own offset, so `out` may be `in` (decoded in place, each
+ * payload left at its body's start as after the reference's memmove,
+ * src/curve_mechanism_base.cpp:253-260: a received buffer becomes the
+ * messages' data without a copy, as v2_decoder's zero-copy msg_t slices do,
+ * src/v2_decoder.cpp:88-113) -- and flags_out / status_out are as for zmqg_decode_batch,
  * with the ZMTP frame's MORE / COMMAND bits ORed into flags_out of a
  * decoded frame (msg_t::set_flags ORs, src/msg.cpp:433-436).  result:
  * frames returned, bytes of `in` they cover (an incomplete last frame is
- * left for the next call), payload bytes written, and error = EMSGSIZE when
+ * left for the next call), payload bytes written (their sum), and error = EMSGSIZE when
  * a frame's size exceeds max_msg_size (>= 0; -1 = no limit), where the
  * reference decoder fails (src/v2_decoder.cpp:74-84): the frames before it
  * are returned.  A size above 2^32 - 1 also ends the parse with EMSGSIZE:

@@ -222,11 +222,14 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
                 w[q] = x;
             }
         }
-        uint64_t found[2];
+        uint64_t f0 = 0, f1 = 0; // (at most 2: signatures are >= 8 bytes apart)
         uint32_t cnt = 0;
-        auto at = [&](uint64_t p) {
-            if (p != kZmtpNone && cnt < 2u)
-                found[cnt++] = p; // (at most 2: signatures are >= 8 bytes apart)
+        auto at = [&](uint64_t p) { // (registers only: no dynamically indexed array)
+            if (p != kZmtpNone && cnt < 2u) {
+                f1 = cnt ? p : f1;
+                f0 = cnt ? f0 : p;
+                ++cnt;
+            }
         };
 #define ZMTP_SIG(Q, J)                                                                                           \
     if (__builtin_amdgcn_alignbyte(w[5 + Q], w[4 + Q], J) == 0x53454d07u &&                                      \
@@ -250,10 +253,10 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
 #undef ZMTP_SIG
         uint32_t total;
         const uint32_t off = zmtp_block_excl(cnt, total);
-#pragma unroll
-        for (uint32_t c = 0; c < 2; ++c)
-            if (c < cnt)
-                dst0[base_out + off + c] = found[c];
+        if (cnt > 0u)
+            dst0[base_out + off] = f0;
+        if (cnt > 1u)
+            dst0[base_out + off + 1] = f1;
         base_out += total;
     }
     if (threadIdx.x == 0)
@@ -385,6 +388,7 @@ struct ZmtpWalk {
     int32_t error;               // 0 or EMSGSIZE
     uint32_t extra;              // 1: the last frame is a complete non-MESSAGE frame at `extra_off`
     unsigned long long extra_off;
+    unsigned long long out_bytes; // payload bytes of the returned frames (k_zmtp_frames adds them up)
 };
 
 // Thread 0 walks the chain (see the file comment).  run[2r], run[2r+1]: the
@@ -485,9 +489,11 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, 
                                                               const uint64_t *runpre, const ZmtpWalk *walk,
                                                               uint64_t max_frames, uint64_t *f_off, uint32_t *f_len,
                                                               uint8_t *f_flags, uint32_t *sid_fill, uint32_t sid,
-                                                              uint64_t *psize)
+                                                              uint64_t *out_off, unsigned long long *out_bytes)
 {
     const uint64_t runs = walk->runs, frames = walk->frames, m = *m_p;
+    __shared__ unsigned long long sh_pb[kZmtpThreads / 64];
+    unsigned long long pb = 0; // this thread's payload bytes
     const uint64_t stride = (uint64_t) gridDim.x * kZmtpThreads;
     // padding and the per-frame session over max_frames
     for (uint64_t j = (uint64_t) blockIdx.x * kZmtpThreads + threadIdx.x; j < max_frames; j += stride) {
@@ -496,11 +502,9 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, 
             f_off[j] = 0;
             f_len[j] = 0;
             f_flags[j] = 0;
-            psize[j] = 0;
+            out_off[j] = 0;
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        psize[max_frames] = 0; // the scan's last entry is the total
     if (blockIdx.x == 0 && threadIdx.x == 0 && walk->extra) {
         uint32_t hdr;
         uint64_t size;
@@ -510,11 +514,10 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, 
         f_off[j] = q + hdr;
         f_len[j] = (uint32_t) size;
         f_flags[j] = b[q];
-        psize[j] = size >= 33u ? size - 33u : 0u;
+        out_off[j] = q + hdr;
+        pb += size >= 33u ? size - 33u : 0u;
     }
-    if (runs == 0)
-        return;
-    for (uint64_t k = (uint64_t) blockIdx.x * kZmtpThreads + threadIdx.x; k < m; k += stride) {
+    for (uint64_t k = (uint64_t) blockIdx.x * kZmtpThreads + threadIdx.x; runs > 0 && k < m; k += stride) {
         // the run holding k: last run whose first candidate <= k
         uint64_t lo = 0, hi = runs;
         while (hi - lo > 1) {
@@ -533,7 +536,23 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, 
         f_off[j] = cand[k] + hdr;
         f_len[j] = (uint32_t) size;
         f_flags[j] = b[cand[k]];
-        psize[j] = size >= 33u ? size - 33u : 0u; // payload bytes (the offsets scan)
+        out_off[j] = cand[k] + hdr; // the payload at its body's offset (see zmqg_decode_zmtp)
+        pb += size >= 33u ? size - 33u : 0u;
+    }
+    // the call's payload bytes: one atomic per workgroup (walk->out_bytes
+    // starts at 0, written by the walk)
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1)
+        pb += __shfl_xor(pb, d);
+    if ((threadIdx.x & 63u) == 0)
+        sh_pb[threadIdx.x >> 6] = pb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (uint32_t q = 0; q < kZmtpThreads / 64; ++q)
+            tot += sh_pb[q];
+        if (tot)
+            atomicAdd(out_bytes, tot);
     }
 }
 
@@ -543,7 +562,7 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, 
 // (and, thread 0, the call's result: frames, bytes consumed, payload
 // bytes, error -- one read back, or none for the asynchronous form)
 __global__ void k_zmtp_flags(const ZmtpWalk *walk, uint64_t max_frames, const uint8_t *f_flags, const int32_t *status,
-                             uint8_t *flags_out, const uint64_t *poff, zmqg_zmtp_result *res)
+                             uint8_t *flags_out, zmqg_zmtp_result *res)
 {
     const uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (j == 0) {
@@ -551,7 +570,7 @@ __global__ void k_zmtp_flags(const ZmtpWalk *walk, uint64_t max_frames, const ui
         r.frames = walk->frames;
         r.consumed = walk->consumed;
         r.error = walk->error;
-        r.out_bytes = poff[walk->frames];
+        r.out_bytes = walk->out_bytes;
         *res = r;
     }
     if (j >= max_frames || j >= walk->frames || status[j] != 0)

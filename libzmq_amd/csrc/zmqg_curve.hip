@@ -171,8 +171,6 @@ struct ZmtpWs {
     uint64_t *first_seg = nullptr;        // [c_cap / 256 + 1] first unlinked candidate in segments >= s
     uint64_t *run = nullptr;              // [2 (f_cap + 1)]
     uint64_t *runpre = nullptr;           // [f_cap + 1]
-    uint64_t *psize = nullptr;            // [f_cap + 1]
-    uint64_t *poff = nullptr;             // [f_cap + 1]
     uint32_t *sid_fill = nullptr;         // [f_cap]
     uint8_t *fflags = nullptr;            // [f_cap]
     ZmtpWalk *walk = nullptr;
@@ -2007,8 +2005,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
             (void) hipFree(p);
     {
         ZmtpWs &z = ctx->zw;
-        void *zp[] = {z.F,      z.wire_off, z.cand_wg, z.count_wg, z.off_wg,   z.cand,   z.nb,   z.first_seg, z.run,
-                      z.runpre, z.psize,    z.poff,    z.sid_fill, z.fflags,   z.walk,   z.res,  z.temp};
+        void *zp[] = {z.F,      z.wire_off, z.cand_wg,  z.count_wg, z.off_wg, z.cand, z.nb,  z.first_seg, z.run,
+                      z.runpre, z.sid_fill, z.fflags,   z.walk,     z.res,    z.temp};
         for (void *p : zp)
             if (p)
                 (void) hipFree(p);
@@ -2568,7 +2566,6 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         while (cap < max_frames)
             cap *= 2;
         if ((rc = grow(ctx, z.run, 2 * (cap + 1), st)) || (rc = grow(ctx, z.runpre, cap + 1, st)) ||
-            (rc = grow(ctx, z.psize, cap + 1, st)) || (rc = grow(ctx, z.poff, cap + 1, st)) ||
             (rc = grow(ctx, z.sid_fill, cap, st)) || (rc = grow(ctx, z.fflags, cap, st)))
             return rc;
         z.f_cap = cap;
@@ -2580,28 +2577,22 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
     // config-2-sized streams in one pass
     const uint32_t pg = (uint32_t) (ctx->cus > 0 ? 4 * ctx->cus : 1024);
     const uint64_t *m_p = z.off_wg + nwg; // the candidate count, on the device
-    // 1. candidates, in stream order
+    // 1. candidates, in stream order: per-workgroup lists, their counts'
+    // exclusive sum, the lists concatenated
     hipLaunchKernelGGL(k_zmtp_scan, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
                        z.count_wg);
     ZCHECK(ctx, hipGetLastError());
-    // the workgroup counts: one workgroup scans up to 8 per thread; the
-    // payload sizes (max_frames + 1 entries) always go to hipCUB
-    const bool small_scan = nwg <= 8u * kZmtpScan1;
-    size_t tb;
-    {
-        size_t need = 0, need2 = 0;
-        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.count_wg, z.off_wg, (int) (nwg + 1), st));
-        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need2, z.psize, z.poff, (int) (max_frames + 1), st));
-        if ((rc = zmtp_temp(ctx, need > need2 ? need : need2, st)))
-            return rc;
-    }
-    if (small_scan) {
+    if (nwg <= 8u * kZmtpScan1) {
         hipLaunchKernelGGL(k_zmtp_exsum, dim3(1), dim3(kZmtpScan1), 0, st, (const uint64_t *) z.count_wg, nwg,
                            z.off_wg);
         ZCHECK(ctx, hipGetLastError());
     } else {
+        size_t need = 0;
+        ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.count_wg, z.off_wg, (int) (nwg + 1), st));
+        if ((rc = zmtp_temp(ctx, need, st)))
+            return rc;
         ZCHECK(ctx, hipMemsetAsync(z.count_wg + nwg, 0, sizeof(uint64_t), st));
-        tb = z.temp_bytes;
+        size_t tb = z.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.count_wg, z.off_wg, (int) (nwg + 1), st));
     }
     hipLaunchKernelGGL(k_zmtp_compact, dim3(g), dim3(kZmtpThreads), 0, st, (const uint64_t *) z.cand_wg,
@@ -2616,14 +2607,13 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
                        max_frames, (const uint64_t *) z.cand, m_p, (const uint64_t *) z.nb, z.first_seg, z.run,
                        z.runpre, z.walk);
     ZCHECK(ctx, hipGetLastError());
-    // 4. descriptors (empty frames up to max_frames), payload offsets
+    // 4. descriptors (empty frames up to max_frames); each payload goes to
+    // its body's offset in `out`, so no offsets scan is needed
     hipLaunchKernelGGL(k_zmtp_frames, dim3(pg), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand, m_p,
                        (const uint64_t *) z.run, (const uint64_t *) z.runpre, (const ZmtpWalk *) z.walk, max_frames,
-                       frame_in_off, frame_len, z.fflags, z.sid_fill, sid, z.psize);
+                       frame_in_off, frame_len, z.fflags, z.sid_fill, sid, out_off,
+                       (unsigned long long *) ((char *) z.walk + offsetof(ZmtpWalk, out_bytes)));
     ZCHECK(ctx, hipGetLastError());
-    tb = z.temp_bytes;
-    ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.psize, z.poff, (int) (max_frames + 1), st));
-    ZCHECK(ctx, hipMemcpyAsync(out_off, z.poff, max_frames * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
     // the decode over max_frames (the empty frames fail as malformed and
     // write nothing else); a maxmsgsize within the frame kernel's range bounds
     // every frame, so the large-frame launches are skipped
@@ -2631,13 +2621,13 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
     o.size = sizeof o;
     if (max_msg_size >= 0 && (uint64_t) max_msg_size <= kMaxFrameStream)
         o.max_len = max_msg_size > 0 ? (uint64_t) max_msg_size : 1u;
-    rc = zmqg_decode_batch_ex(ctx, max_frames, z.sid_fill, frame_in_off, frame_len, in, z.poff, out, flags_out,
+    rc = zmqg_decode_batch_ex(ctx, max_frames, z.sid_fill, frame_in_off, frame_len, in, out_off, out, flags_out,
                               status_out, o.max_len ? &o : nullptr, stream);
     if (rc)
         return rc;
     hipLaunchKernelGGL(k_zmtp_flags, dim3((unsigned) ((max_frames + 255) / 256)), dim3(256), 0, st,
                        (const ZmtpWalk *) z.walk, max_frames, (const uint8_t *) z.fflags, (const int32_t *) status_out,
-                       flags_out, (const uint64_t *) z.poff, result);
+                       flags_out, result);
     ZCHECK(ctx, hipGetLastError());
     return 0;
 }

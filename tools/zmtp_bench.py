@@ -88,7 +88,7 @@ def main():
         d.set_peer_nonce(0, 2)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        r = d.decode_zmtp(0, framed, total, -1, n, d_foff, d_flen, d_poff, back, fl, st)
+        r = d.decode_zmtp(0, framed, total, -1, n, d_foff, d_flen, d_poff, zback, fl, st)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         assert r["frames"] == n and r["consumed"] == total and r["error"] == 0
@@ -98,9 +98,12 @@ def main():
     torch.cuda.synchronize()
     d_batch()
     tb = min(d_batch() for _ in range(5)) * 1e6
+    assert int((st != 0).sum()) == 0 and torch.equal(back, pay)
+    zback = torch.zeros(total, dtype=torch.uint8, device=dev)  # payloads at their bodies' offsets
     d_zmtp()
     tzd = min(d_zmtp() for _ in range(5)) * 1e6
-    assert int((st != 0).sum()) == 0 and torch.equal(back, pay)
+    idx = d_poff[:, None] + torch.arange(P, device=dev)[None, :]
+    assert int((st != 0).sum()) == 0 and torch.equal(zback[idx].reshape(-1), pay)
     print(f"decode_batch {tb:8.1f} us   decode_zmtp {tzd:8.1f} us  (parse + decode, synchronous)")
 
 
