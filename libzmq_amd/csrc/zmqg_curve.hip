@@ -2278,7 +2278,8 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     rp.psnap = w.psnap;
     rp.peer = ctx->peer;
     if (multi) {
-        rp.iota = w.iota;
+        if (ctx->max_sessions > kReplayMaxSessions)
+            rp.iota = w.iota; // (the sort fallback's values)
         if (smax)
             ZCHECK(ctx, hipMemsetAsync(smax, 0, sizeof(unsigned long long) * ctx->max_sessions, st));
     } else {

@@ -420,12 +420,13 @@ def test_fresh_ctx_decodes_at_once_on_nonblocking_stream(torch_cuda, C):
 
 
 # ------------------------------------------------------------------ replay tables
-@pytest.mark.parametrize("n_sessions,n", [(1000, 40000), (37, 9000), (9000, 3000)])
+@pytest.mark.parametrize("n_sessions,n", [(1000, 40000), (37, 9000), (9000, 3000), (1, 300000)])
 def test_multi_session_replay_vs_oracle(torch_cuda, C, n_sessions, n):
     """Random session order (sessions repeating inside a wave), random
     nonce gaps and replays, forged headers: statuses, flags, payloads and
     final peer nonces equal the oracle's sequential decode (9000 sessions: the
-    sort fallback)."""
+    sort fallback; one session over 300,000 frames: a grid larger than the
+    device, so the in-kernel look-back over workgroup tickets)."""
     torch = torch_cuda
     rng = np.random.default_rng(n_sessions)
     keys = _keys(rng, n_sessions)
