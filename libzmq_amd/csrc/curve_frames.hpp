@@ -38,15 +38,12 @@
 #pragma once
 
 #ifndef ZMQG_FRAMES_ABLATE
-#define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: k_frames: 1 no Poly1305, 2 no stores, 4 no input shift; k_frames_seq: 8 no stores, 16 no loads, 32 no Salsa20, 64 no Poly1305
+#define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: k_frames: 1 no Poly1305, 2 no stores, 4 no input shift; k_frames_seq: 8 no stores, 16 no loads, 32 no Salsa20, 64 no Poly1305, 128 stores to 64-byte-aligned places (whole lines), 256 loads from 64-byte-aligned places
 #endif
 
-#ifndef ZMQG_SEQ_DEPTH
-#define ZMQG_SEQ_DEPTH 1 // k_frames_seq: windows of input in flight ahead of the one being processed (1 or 2)
-#endif
 
-#ifndef ZMQG_SEQ_PAIRST
-#define ZMQG_SEQ_PAIRST 0 // k_frames_seq: store windows in pairs
+#ifndef ZMQG_SEQ_AL64
+#define ZMQG_SEQ_AL64 1 // k_frames_seq decode: 64-byte payload chunks when every payload of a wave starts 64-byte aligned (0: off, for timing)
 #endif
 
 #ifndef ZMQG_FR_BS
@@ -183,7 +180,15 @@ __device__ __forceinline__ void frame_store(uint64_t B, uint32_t w, uint32_t S, 
                                             bool last)
 {
     const uint32_t u = (uint32_t) B & 3u, up = u ? u : 4u, sh = 4u - up;
-    const uint64_t a = B - up + 64ull * w; // aligned
+    // (ablation 128, timing only: every window stored whole to a 64-byte-aligned
+    // place, so a frame's consecutive windows fill whole 128-byte lines)
+    const uint64_t a = (ZMQG_FRAMES_ABLATE & 128) ? ((B + 160ull) & ~127ull) + 64ull * w : B - up + 64ull * w; // aligned
+    if (ZMQG_FRAMES_ABLATE & 128) {
+        if (a + 64ull > B + S) // (never beyond the frame's own end)
+            return;
+        S = 0xffffffffu;
+        last = false;
+    }
     uint32_t o[17];
     o[0] = __builtin_amdgcn_alignbyte(y[0], yprev, sh);
 #pragma unroll
@@ -362,6 +367,57 @@ __device__ __forceinline__ uint64_t nonce_base(const FrameCtl &ctl)
     return ctl.nonce_ctr ? __hip_atomic_load(ctl.nonce_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
 }
 
+// A frame kernel's view of the call state (ZState), taken by thread 0 of
+// each workgroup at its start: the epoch, its look-back ticket (ticket:
+// true) and the encode nonce base.  Right after these reads have returned
+// the workgroup counts itself in zs->done; the one that completes the count
+// has every other workgroup's reads behind it, so it may reset the counters
+// and advance the epoch and the send counter for the next call
+// (call_state_end; the next call is stream-ordered after this one, and
+// nothing in this launch reads zs->epoch / ticket / done or the counter
+// after its start).  The count's return value is only looked at in
+// call_state_end, so no workgroup waits for the atomic: round 1 counted
+// workgroups at their end, which put a device-scope round trip on every
+// workgroup's exit path.
+struct CallState {
+    uint32_t epoch, ticket;
+    uint64_t nbase;
+    uint32_t done_old; // thread 0 only: zs->done before this workgroup's count
+};
+
+template <bool DEC>
+__device__ __forceinline__ CallState call_state_begin(ZState *zs, const FrameCtl &ctl, bool ticket)
+{
+    __shared__ CallState sh_cs;
+    uint32_t done_old = 0;
+    if (threadIdx.x == 0) {
+        CallState c;
+        c.epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c.ticket = ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
+        c.nbase = DEC ? 0ull : nonce_base(ctl);
+        c.done_old = 0;
+        sh_cs = c;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the reads above have returned
+        done_old = atomicAdd(&zs->done, 1u);
+    }
+    __syncthreads();
+    CallState c = sh_cs;
+    c.done_old = done_old;
+    return c;
+}
+
+template <bool DEC>
+__device__ __forceinline__ void call_state_end(ZState *zs, const FrameCtl &ctl, const CallState &c, uint32_t n)
+{
+    if (threadIdx.x == 0 && c.done_old + 1u == gridDim.x) {
+        __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&zs->epoch, c.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!DEC && ctl.nonce_ctr)
+            __hip_atomic_store(ctl.nonce_ctr, c.nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Frames whose region a failing lane zero-fills itself; longer ones go to
 // the post list (k_post spreads them over the whole grid).
 constexpr uint32_t kLaneFillMax = 4608;
@@ -453,7 +509,7 @@ __device__ __forceinline__ void fail_unprocessed(int32_t status, uint32_t L_in, 
 
 // No big-frame handler (tools, tests): frames above max_stream are skipped.
 struct NoBigFrames {
-    __device__ void operator()(uint32_t, unsigned long long *) const {}
+    __device__ void operator()(uint32_t, unsigned long long *, uint64_t) const {}
 };
 
 // Frame kernel.  DEC = decode.  Frames whose stream is longer than
@@ -477,20 +533,12 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
         clk0 = __builtin_amdgcn_s_memtime();
         rclk0 = __builtin_amdgcn_s_memrealtime();
     }
-    uint32_t wg = blockIdx.x;
-    __shared__ uint32_t sh_ticket, sh_epoch;
     __shared__ unsigned long long sh_wmax[kFramesWaves];
-    if (threadIdx.x == 0) {
-        // the epoch first: it only advances after every workgroup has finished
-        sh_epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lb && !rp.ordered && !(rp.dbg & 2))
-            sh_ticket = atomicAdd(&zs->ticket, 1u);
-    }
-    __syncthreads();
-    const uint32_t epoch = sh_epoch;
-    if (lb && !rp.ordered && !(rp.dbg & 2))
-        wg = sh_ticket;
-    const uint64_t nbase = DEC ? 0ull : nonce_base(ctl);
+    const bool use_ticket = lb && !rp.ordered && !(rp.dbg & 2);
+    const CallState cs = call_state_begin<DEC>(zs, ctl, use_ticket);
+    const uint32_t epoch = cs.epoch;
+    const uint32_t wg = use_ticket ? cs.ticket : blockIdx.x;
+    const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0; // the next call's list (the previous body has finished with it)
@@ -553,7 +601,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     if (DEC) {
         vn = valid && q == 0 && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
         psn = rp.peer[s];
-        if (valid && q == 0) {
+        if (valid && q == 0 && !lb) { // (several sessions: the replay tables' input)
             rp.vout[i] = vn;
             rp.psnap[i] = psn;
             if (rp.iota)
@@ -876,9 +924,11 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
             excl = psn;
     }
     if (is_big && q == 0 && !ctl.no_body) {
-        if (lb)
+        if (lb) { // the body's finisher applies the rule to this frame
             rp.excl[i] = excl;
-        big(i, list_ctr);
+            rp.psnap[i] = psn;
+        }
+        big(i, list_ctr, nbase);
     }
     if (rp.clk && threadIdx.x == 0) {
         unsigned long long *c = rp.clk + 4ull * blockIdx.x;
@@ -888,19 +938,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
         c[3] = ((unsigned long long) __builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
                __builtin_amdgcn_s_getreg((31 << 11) | 4); // XCC_ID : HW_ID
     }
-    // the last workgroup to get here resets the counters and advances the
-    // epoch for the next call (every workgroup has read epoch and ticket)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this workgroup's list appends are done
-        if (atomicAdd(&zs->done, 1u) + 1u == gridDim.x) {
-            __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!DEC && ctl.nonce_ctr) // every workgroup has read the counter
-                __hip_atomic_store(ctl.nonce_ctr, nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    call_state_end<DEC>(zs, ctl, cs, n);
     if (!DEC && valid && q == 0 && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
     if (!valid || q != 0 || !small)
@@ -950,7 +988,8 @@ __device__ __forceinline__ bool frame_prefetch(uint64_t A4, uint32_t lim, uint64
     const uint64_t a = A4 + 64ull * w;
     const bool ok = 64u * w + 68u <= lim || a + 68ull <= wave_end;
     if (ok) {
-        const GCU4a4 *p = (const GCU4a4 *) (uintptr_t) (a + 4ull);
+        // (ablation 256, timing only: the 64 bytes read from the 64-byte-aligned place below)
+        const GCU4a4 *p = (const GCU4a4 *) (uintptr_t) ((ZMQG_FRAMES_ABLATE & 256) ? (a & ~63ull) : a + 4ull);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const u32x4 tt = p[k];
@@ -1009,19 +1048,11 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
 {
     const bool lb = DEC && rp.lb_flag != nullptr;
     SEQ_STAMP(0u);
-    uint32_t wg = blockIdx.x;
-    __shared__ uint32_t sh_ticket, sh_epoch;
     __shared__ unsigned long long sh_wmax[kFramesWaves];
-    if (threadIdx.x == 0) {
-        sh_epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lb && !rp.ordered)
-            sh_ticket = atomicAdd(&zs->ticket, 1u);
-    }
-    __syncthreads();
-    const uint32_t epoch = sh_epoch;
-    if (lb && !rp.ordered)
-        wg = sh_ticket;
-    const uint64_t nbase = DEC ? 0ull : nonce_base(ctl);
+    const CallState cs = call_state_begin<DEC>(zs, ctl, lb && !rp.ordered);
+    const uint32_t epoch = cs.epoch;
+    const uint32_t wg = lb && !rp.ordered ? cs.ticket : blockIdx.x;
+    const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
@@ -1090,7 +1121,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     if (DEC) {
         vn = valid && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
         psn = rp.peer[s];
-        if (valid) {
+        if (valid && !lb) { // (several sessions: the replay tables' input)
             rp.vout[i] = vn;
             rp.psnap[i] = psn;
             if (rp.iota)
@@ -1144,13 +1175,17 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     // alternate between the two buffers
     uint32_t ddA[16], ddB[16];
     bool fastA = nw > 1u ? frame_prefetch(A4, lim, wave_end, 1u, ddA) : true, fastB = true;
-#if ZMQG_SEQ_DEPTH == 2
-    // two windows in flight: windows t, t+1, t+2 rotate through three buffers
-    uint32_t ddC[16];
-    bool fastC = true;
-    if (nw > 2u)
-        fastB = frame_prefetch(A4, lim, wave_end, 2u, ddB);
-#endif
+
+    // Decode output in 64-byte payload chunks when every lane's payload
+    // starts on a 64-byte boundary (wave-uniform; e.g. packed 1 KiB
+    // payloads): chunk c, payload bytes [64c, 64c+64) = stream bytes
+    // [64c+33, 64c+97), leaves in step c+1 from windows c (yp) and c+1 as
+    // four dwordx4 on one aligned 64-byte piece, so a frame's consecutive
+    // steps fill whole 128-byte lines.  Otherwise each window's 64 output
+    // bytes go out at their own alignment (frame_store), two partial lines
+    // per window.
+    const bool al64 = ZMQG_SEQ_AL64 && DEC && __builtin_amdgcn_ballot_w64(((uint32_t) (uintptr_t) dst & 63u) != 0u) == 0;
+    uint32_t yp[16]; // al64: the previous window's output words
 
     SEQ_STAMP(1u);
     // ---- step 0: window 0 (Poly1305 key, first 32 ciphertext bytes, header)
@@ -1204,6 +1239,9 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             cp[k] = DEC ? x[k] : y[k];
         cp_len = (S < 64u ? S : 64u) - 32u; // (S = 0: unused)
         ycarry = y[15];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            yp[k] = y[k];
         if (nw > 0) {
             if (DEC) {
                 fl = y[8] & 3u;
@@ -1216,7 +1254,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
 #pragma unroll
                 for (int k = 8; k < 16; ++k)
                     pay[k] = 0;
-                store_window(dst, (int) (S < 64u ? S : 64u) - 33, pay);
+                if (!al64 || nw == 1u) // (al64: chunk 0 goes out with window 1)
+                    store_window(dst, (int) (S < 64u ? S : 64u) - 33, pay);
             } else {
                 uint32_t o[16];
                 o[0] = 0x53454d07u; // "\x07MESSAGE" || nonce
@@ -1240,9 +1279,6 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     // ---- steps 1 ..: window t (words in dd, prefetched by the previous
     // step; the two buffers alternate so that the loads keep their register
     // tuples)
-#if ZMQG_SEQ_PAIRST
-    uint32_t ysv[16], ysv_prev = 0; // an odd window's output, stored with the next one
-#endif
     auto step = [&](uint32_t t, uint32_t (&dd)[16], bool &fast, uint32_t (&dn)[16], bool &fastn) {
         SEQ_STAMP(3u + t);
         const bool act = t < nw;
@@ -1338,56 +1374,78 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             for (int k = 0; k < 16; ++k)
                 dn[k] = y[k] + k;
             fastn = true;
-        } else if (t + ZMQG_SEQ_DEPTH < nw) {
-            fastn = frame_prefetch(A4, lim, wave_end, t + ZMQG_SEQ_DEPTH, dn);
+        } else if (t + 1u < nw) {
+            fastn = frame_prefetch(A4, lim, wave_end, t + 1u, dn);
         }
         if (t < 8u)
             SEQ_STAMP(52u + t);
         if (ZMQG_FRAMES_ABLATE & 8) {
             if (act && y[3] == 0x12345678u && y[7] == ycarry)
                 *(GU32 *) (uintptr_t) B = y[0];
-        } else {
-#if ZMQG_SEQ_PAIRST
-            // windows go out in pairs (t-1, t at even t): a lane's 128
-            // contiguous bytes in consecutive instructions, so both halves of
-            // a 128-byte line reach L2 together
-            if ((t & 1u) && t + 1u < steps) {
+        } else if (DEC && al64) {
+            // payload chunk t-1 (windows t-1 and t); on a lane's last window
+            // also what is left of the payload (chunk t, window t alone)
+            uint32_t o[16];
 #pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    ysv[k] = y[k];
-                ysv_prev = ycarry;
+            for (int k = 0; k < 7; ++k)
+                o[k] = __builtin_amdgcn_alignbyte(yp[9 + k], yp[8 + k], 1);
+            o[7] = __builtin_amdgcn_alignbyte(y[0], yp[15], 1);
+#pragma unroll
+            for (int k = 8; k < 16; ++k)
+                o[k] = __builtin_amdgcn_alignbyte(y[k - 7], y[k - 8], 1);
+            uint8_t *const cdst = dst + 64u * (t - 1u);
+            const bool lastw = act && t + 1u == nw;
+            if (__builtin_amdgcn_ballot_w64(lastw) == 0) {
+                if (act) {
+                    GU4 *const q = (GU4 *) (uintptr_t) cdst;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        q[k] = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                }
             } else {
-                if ((t & 1u) == 0 && t - 1u < nw)
-                    frame_store(B, t - 1u, S, ysv, ysv_prev, t == nw);
-                if (act)
-                    frame_store(B, t, S, y, ycarry, t + 1u == nw);
+                const uint32_t P = S - 33u; // (act: S >= 64t + 1 > 33)
+                if (act) {
+                    const uint32_t r = P - 64u * (t - 1u);
+                    store_window(cdst, (int) (r < 64u ? r : 64u), o);
+                }
+                if (lastw && P > 64u * t) {
+                    uint32_t o2[16];
+#pragma unroll
+                    for (int k = 0; k < 7; ++k)
+                        o2[k] = __builtin_amdgcn_alignbyte(y[9 + k], y[8 + k], 1);
+                    o2[7] = __builtin_amdgcn_alignbyte(0u, y[15], 1);
+#pragma unroll
+                    for (int k = 8; k < 16; ++k)
+                        o2[k] = 0;
+                    store_window(cdst + 64, (int) (P - 64u * t), o2);
+                }
             }
-#else
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                yp[k] = y[k];
+        } else {
             if (act)
                 frame_store(B, t, S, y, ycarry, t + 1u == nw);
-#endif
         }
         ycarry = y[15];
         if (t < 8u)
             SEQ_STAMP(36u + t);
     };
-#if ZMQG_SEQ_DEPTH == 2
+    // (both exits leave the loop: a skipped second step reaching the back
+    // edge would leave buffer B's loads outstanding at the loop head as far
+    // as the compiler's wait analysis knows, and every step would then wait
+    // for all loads before its first write of a buffer register)
+    if (steps > 1u) {
 #pragma unroll 1
-    for (uint32_t t = 1; t < steps; t += 3) {
-        step(t, ddA, fastA, ddC, fastC);
-        if (t + 1u < steps)
+        for (uint32_t t = 1;; t += 2) {
+            step(t, ddA, fastA, ddB, fastB);
+            if (t + 1u >= steps)
+                break;
             step(t + 1u, ddB, fastB, ddA, fastA);
-        if (t + 2u < steps)
-            step(t + 2u, ddC, fastC, ddB, fastB);
+            if (t + 2u >= steps)
+                break;
+        }
     }
-#else
-#pragma unroll 1
-    for (uint32_t t = 1; t < steps; t += 2) {
-        step(t, ddA, fastA, ddB, fastB);
-        if (t + 1u < steps)
-            step(t + 1u, ddB, fastB, ddA, fastA);
-    }
-#endif
     SEQ_STAMP(60u);
     // the last window's MAC
     if (steps > 0 && nw == steps)
@@ -1410,21 +1468,13 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             excl = psn;
     }
     if (is_big && !ctl.no_body) {
-        if (lb)
+        if (lb) { // the body's finisher applies the rule to this frame
             rp.excl[i] = excl;
-        big(i, list_ctr);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(&zs->done, 1u) + 1u == gridDim.x) {
-            __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!DEC && ctl.nonce_ctr) // every workgroup has read the counter
-                __hip_atomic_store(ctl.nonce_ctr, nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rp.psnap[i] = psn;
         }
+        big(i, list_ctr, nbase);
     }
+    call_state_end<DEC>(zs, ctl, cs, n);
     SEQ_STAMP(61u);
     if (!DEC && valid && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;

@@ -109,19 +109,11 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     __shared__ __attribute__((aligned(16))) uint8_t st_lds[kFramesWaves * kStWave];
     const bool lb = DEC && rp.lb_flag != nullptr;
     SEQ_STAMP(0u);
-    uint32_t wg = blockIdx.x;
-    __shared__ uint32_t sh_ticket, sh_epoch;
     __shared__ unsigned long long sh_wmax[kFramesWaves];
-    if (threadIdx.x == 0) {
-        sh_epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lb && !rp.ordered)
-            sh_ticket = atomicAdd(&zs->ticket, 1u);
-    }
-    __syncthreads();
-    const uint32_t epoch = sh_epoch;
-    if (lb && !rp.ordered)
-        wg = sh_ticket;
-    const uint64_t nbase = DEC ? 0ull : nonce_base(ctl);
+    const CallState cs = call_state_begin<DEC>(zs, ctl, lb && !rp.ordered);
+    const uint32_t epoch = cs.epoch;
+    const uint32_t wg = lb && !rp.ordered ? cs.ticket : blockIdx.x;
+    const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
@@ -187,7 +179,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     if (DEC) {
         vn = valid && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
         psn = rp.peer[s];
-        if (valid) {
+        if (valid && !lb) { // (several sessions: the replay tables' input)
             rp.vout[i] = vn;
             rp.psnap[i] = psn;
             if (rp.iota)
@@ -511,21 +503,13 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
             excl = psn;
     }
     if (is_big && !ctl.no_body) {
-        if (lb)
+        if (lb) { // the body's finisher applies the rule to this frame
             rp.excl[i] = excl;
-        big(i, list_ctr);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(&zs->done, 1u) + 1u == gridDim.x) {
-            __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&zs->epoch, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!DEC && ctl.nonce_ctr) // every workgroup has read the counter
-                __hip_atomic_store(ctl.nonce_ctr, nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rp.psnap[i] = psn;
         }
+        big(i, list_ctr, nbase);
     }
+    call_state_end<DEC>(zs, ctl, cs, n);
     SEQ_STAMP(61u);
     if (!DEC && valid && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;

@@ -382,10 +382,10 @@ struct EncodeHead {
     uint32_t max_sessions;
     BigRecords R;
     const unsigned long long *nonce_ctr; // ZMQG_OPT_NONCE_AUTO, one session (FrameCtl::nonce_ctr)
-    __device__ void operator()(uint32_t i, unsigned long long *list_ctr) const;
+    __device__ void operator()(uint32_t i, unsigned long long *list_ctr, uint64_t nbase) const;
 };
 
-__device__ void EncodeHead::operator()(uint32_t i, unsigned long long *list_ctr) const
+__device__ void EncodeHead::operator()(uint32_t i, unsigned long long *list_ctr, uint64_t nbase) const
 {
     FrameHot *hot = R.hot;
     FramePow *pw = R.pw;
@@ -406,8 +406,9 @@ __device__ void EncodeHead::operator()(uint32_t i, unsigned long long *list_ctr)
 #pragma unroll
     for (int t = 0; t < 8; ++t)
         H.key[t] = ses.enc_key[t];
-    const uint64_t nc =
-        nonce_ctr ? __hip_atomic_load(nonce_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + i : nonce[i];
+    // (the counter as the frame kernel read it at its start: the workgroup
+    // completing the call count advances it for the next call)
+    const uint64_t nc = nonce_ctr ? nbase + i : nonce[i];
     const uint32_t n0 = bswap32((uint32_t) (nc >> 32)), n1 = bswap32((uint32_t) nc);
 
     uint32_t ks[16];
@@ -550,10 +551,10 @@ struct DecodeHead {
     const DevSession *sessions;
     uint32_t max_sessions;
     BigRecords R;
-    __device__ void operator()(uint32_t i, unsigned long long *list_ctr) const;
+    __device__ void operator()(uint32_t i, unsigned long long *list_ctr, uint64_t nbase) const;
 };
 
-__device__ void DecodeHead::operator()(uint32_t i, unsigned long long *list_ctr) const
+__device__ void DecodeHead::operator()(uint32_t i, unsigned long long *list_ctr, uint64_t) const
 {
     FrameHot *hot = R.hot;
     FramePow *pw = R.pw;
