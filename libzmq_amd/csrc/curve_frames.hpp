@@ -369,47 +369,52 @@ __device__ __forceinline__ uint64_t nonce_base(const FrameCtl &ctl)
 
 // A frame kernel's view of the call state (ZState), taken by thread 0 of
 // each workgroup at its start: the epoch, its look-back ticket (ticket:
-// true) and the encode nonce base.  Right after these reads have returned
-// the workgroup counts itself in zs->done; the one that completes the count
-// has every other workgroup's reads behind it, so it may reset the counters
-// and advance the epoch and the send counter for the next call
-// (call_state_end; the next call is stream-ordered after this one, and
-// nothing in this launch reads zs->epoch / ticket / done or the counter
-// after its start).  The count's return value is only looked at in
-// call_state_end, so no workgroup waits for the atomic: round 1 counted
-// workgroups at their end, which put a device-scope round trip on every
-// workgroup's exit path.
+// true) and the encode nonce base.  Once these reads have been used (after
+// its first window) the workgroup counts itself in zs->done with a
+// fire-and-forget atomic (call_state_count); workgroup 0, at its end, waits
+// for the count to reach the grid and then resets the counters and advances
+// the epoch and the send counter for the next call (call_state_end: every
+// other workgroup has read them by then; the next call is stream-ordered
+// after this one; nothing in this launch reads them after its start).  So no
+// workgroup waits on a returning device-scope atomic: round 1 counted at
+// every workgroup's end with one (a round trip on each exit path), and
+// counting at the start with one serialised the whole grid's first
+// workgroups behind 256 atomics on one address (tools/seq_stamps.hip).
+// Workgroup 0 is dispatched first, so the count is normally complete when
+// it looks, and its one extra load falls inside the other workgroups' time.
 struct CallState {
     uint32_t epoch, ticket;
     uint64_t nbase;
-    uint32_t done_old; // thread 0 only: zs->done before this workgroup's count
 };
 
 template <bool DEC>
 __device__ __forceinline__ CallState call_state_begin(ZState *zs, const FrameCtl &ctl, bool ticket)
 {
     __shared__ CallState sh_cs;
-    uint32_t done_old = 0;
     if (threadIdx.x == 0) {
         CallState c;
         c.epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         c.ticket = ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
         c.nbase = DEC ? 0ull : nonce_base(ctl);
-        c.done_old = 0;
         sh_cs = c;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the reads above have returned
-        done_old = atomicAdd(&zs->done, 1u);
     }
     __syncthreads();
-    CallState c = sh_cs;
-    c.done_old = done_old;
-    return c;
+    return sh_cs;
+}
+
+// (called once the CallState values have been used, so its reads are done)
+__device__ __forceinline__ void call_state_count(ZState *zs)
+{
+    if (threadIdx.x == 0)
+        (void) __hip_atomic_fetch_add(&zs->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool DEC>
 __device__ __forceinline__ void call_state_end(ZState *zs, const FrameCtl &ctl, const CallState &c, uint32_t n)
 {
-    if (threadIdx.x == 0 && c.done_old + 1u == gridDim.x) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        while (__hip_atomic_load(&zs->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x)
+            __builtin_amdgcn_s_sleep(2);
         __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&zs->epoch, c.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -659,6 +664,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     uint32_t dn[17]; // raw input words of this lane's next window, loaded a step ahead
     if (nst > 0 && !(q == 0 && !DEC)) // encode's window 0 reads the payload itself
         frame_load_raw(A, q, S, dn);
+    call_state_count(zs);
 
 #pragma unroll 1
     for (uint32_t t = 0; t < steps; ++t) {
@@ -1275,6 +1281,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
         }
     }
     SEQ_STAMP(2u);
+    call_state_count(zs);
 
     // ---- steps 1 ..: window t (words in dd, prefetched by the previous
     // step; the two buffers alternate so that the loads keep their register

@@ -379,6 +379,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         ring_put(0u, y);
     }
     SEQ_STAMP(2u);
+    call_state_count(zs);
 
     // ---- steps 1 ..: window t
 #pragma unroll 1

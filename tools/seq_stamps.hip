@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <vector>
 #include <algorithm>
+#include <math.h>
 #include "../libzmq_amd/csrc/curve_frames_lds.hpp"
 #ifndef STAMP_LDS
 #define STAMP_LDS 0 // 1: stamp k_frames_lds instead of k_frames_seq
@@ -117,6 +118,68 @@ int main()
                 continue;
             std::sort(v.begin(), v.end());
             printf("  slot %2d: %8lld %8lld %8lld\n", sl, v.front(), v[v.size() / 2], v.back());
+        }
+        // wave durations (entry -> slot 61) by workgroup % 8 (the XCD of a
+        // round-robin dispatch), by wave in workgroup, and by grid position
+        {
+            double sx[8] = {0}, nx[8] = {0}, sw[4] = {0}, nwv[4] = {0}, sq[8] = {0}, nq[8] = {0};
+            std::vector<long long> all;
+            for (size_t w = 0; w < nwaves; ++w) {
+                if (!c[64 * w + 61])
+                    continue;
+                const double d = (double) (c[64 * w + 61] - c[64 * w]);
+                const size_t b = w / kFramesWaves;
+                sx[b % 8] += d, nx[b % 8] += 1;
+                sw[w % kFramesWaves] += d, nwv[w % kFramesWaves] += 1;
+                sq[b * 8 / (nwaves / kFramesWaves)] += d, nq[b * 8 / (nwaves / kFramesWaves)] += 1;
+                all.push_back((long long) d);
+            }
+            std::sort(all.begin(), all.end());
+            printf("  duration p10/p50/p90/p99/max: %lld %lld %lld %lld %lld\n", all[all.size() / 10],
+                   all[all.size() / 2], all[all.size() * 9 / 10], all[all.size() * 99 / 100], all.back());
+            printf("  mean by block%%8:");
+            for (int k = 0; k < 8; ++k)
+                printf(" %.0f", sx[k] / (nx[k] ? nx[k] : 1));
+            printf("\n  mean by wave in block:");
+            for (uint32_t k = 0; k < kFramesWaves; ++k)
+                printf(" %.0f", sw[k] / (nwv[k] ? nwv[k] : 1));
+            printf("\n  mean by grid eighth:");
+            for (int k = 0; k < 8; ++k)
+                printf(" %.0f", sq[k] / (nq[k] ? nq[k] : 1));
+            printf("\n");
+            // spread of the workgroup means (a CU-wide effect) against the
+            // spread inside workgroups (a wave's own)
+            double s1 = 0, s2 = 0, w2 = 0, mu = 0;
+            size_t nb = nwaves / kFramesWaves;
+            std::vector<double> bm(nb, 0.0);
+            for (size_t b = 0; b < nb; ++b) {
+                for (uint32_t k = 0; k < kFramesWaves; ++k)
+                    bm[b] += (double) (c[64 * (b * kFramesWaves + k) + 61] - c[64 * (b * kFramesWaves + k)]);
+                bm[b] /= kFramesWaves;
+                mu += bm[b] / nb;
+            }
+            for (size_t b = 0; b < nb; ++b) {
+                s1 += (bm[b] - mu) * (bm[b] - mu) / nb;
+                for (uint32_t k = 0; k < kFramesWaves; ++k) {
+                    const double d = (double) (c[64 * (b * kFramesWaves + k) + 61] - c[64 * (b * kFramesWaves + k)]);
+                    w2 += (d - bm[b]) * (d - bm[b]) / (nb * kFramesWaves);
+                    s2 += (d - mu) * (d - mu) / (nb * kFramesWaves);
+                }
+            }
+            std::vector<double> sb = bm;
+            std::sort(sb.begin(), sb.end());
+            printf("  sd all %.0f, sd of workgroup means %.0f, sd within workgroups %.0f; workgroup means p50 %.0f "
+                   "p90 %.0f max %.0f\n",
+                   sqrt(s2), sqrt(s1), sqrt(w2), sb[nb / 2], sb[nb * 9 / 10], sb.back());
+            // per-step time of the slowest and the median waves (slot 5 -> slot 19)
+            std::vector<long long> st;
+            for (size_t w = 0; w < nwaves; ++w)
+                if (c[64 * w + 19] && c[64 * w + 5])
+                    st.push_back((long long) (c[64 * w + 19] - c[64 * w + 5]));
+            std::sort(st.begin(), st.end());
+            if (!st.empty())
+                printf("  steps 2..15 per step: p50 %lld p90 %lld max %lld\n", st[st.size() / 2] / 14,
+                       st[st.size() * 9 / 10] / 14, st.back() / 14);
         }
     }
     return 0;
