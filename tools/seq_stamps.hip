@@ -15,6 +15,9 @@
 #include <algorithm>
 #include <math.h>
 #include "../libzmq_amd/csrc/curve_frames_lds.hpp"
+#ifndef STAMP_SHMEM_KB
+#define STAMP_SHMEM_KB 0 // dynamic LDS requested per workgroup (unused; 84: one workgroup per CU)
+#endif
 #ifndef STAMP_LDS
 #define STAMP_LDS 0 // 1: stamp k_frames_lds instead of k_frames_seq
 #endif
@@ -80,11 +83,11 @@ int main()
             CHECK(hipMemset(d_clk, 0, 8 * 64 * nwaves));
             rp.clk = rep == 2 ? d_clk : nullptr;
             if (!dec)
-                hipLaunchKernelGGL((KFR<false, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid, d_nonce,
+                hipLaunchKernelGGL((KFR<false, NoBigFrames>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid, d_nonce,
                                    d_flags, d_ioff, d_len, d_pay, d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr,
                                    nullptr, rp, NoBigFrames{}, d_zs, FrameCtl{});
             else
-                hipLaunchKernelGGL((KFR<true, NoBigFrames>), grid, dim3(kFramesBS), 0, 0, n, d_sid,
+                hipLaunchKernelGGL((KFR<true, NoBigFrames>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid,
                                    (const uint64_t *) nullptr, (const uint8_t *) nullptr, d_ooff, d_wl, d_wire, d_ioff,
                                    d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, NoBigFrames{}, d_zs, FrameCtl{});
             CHECK(hipDeviceSynchronize());
@@ -180,6 +183,29 @@ int main()
             if (!st.empty())
                 printf("  steps 2..15 per step: p50 %lld p90 %lld max %lld\n", st[st.size() / 2] / 14,
                        st[st.size() * 9 / 10] / 14, st.back() / 14);
+            // the slowest tenth of the waves against the middle fifth: per step
+            // (2..15) keystream+MAC (slot 3+t -> 24+t) and the rest
+            std::vector<std::pair<long long, size_t>> dw;
+            for (size_t w = 0; w < nwaves; ++w)
+                dw.push_back({(long long) (c[64 * w + 61] - c[64 * w]), w});
+            std::sort(dw.begin(), dw.end());
+            auto band = [&](size_t lo, size_t hi, const char *name) {
+                double ks = 0, rest = 0, pro = 0, epi = 0;
+                for (size_t j = lo; j < hi; ++j) {
+                    const size_t w = dw[j].second;
+                    for (int t = 2; t <= 15; ++t) {
+                        ks += (double) (c[64 * w + 24 + t] - c[64 * w + 3 + t]);
+                        rest += (double) (c[64 * w + 3 + t + 1] - c[64 * w + 24 + t]);
+                    }
+                    pro += (double) (c[64 * w + 5] - c[64 * w]);
+                    epi += (double) (c[64 * w + 61] - c[64 * w + 18]);
+                }
+                const double m = (double) (hi - lo);
+                printf("  %s: per step keystream+MAC %.0f, rest %.0f; entry->step 2 %.0f; step 15->end %.0f\n", name,
+                       ks / m / 14, rest / m / 14, pro / m, epi / m);
+            };
+            band(nwaves * 2 / 5, nwaves * 3 / 5, "middle fifth ");
+            band(nwaves * 9 / 10, nwaves, "slowest tenth");
         }
     }
     return 0;
