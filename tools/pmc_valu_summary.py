@@ -12,7 +12,7 @@ acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{sys.argv[1]}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        if "k_frames" not in name:
+        if "k_frames_seq" not in name:  # (the config-2 kernel only)
             continue
         k = "k_frames<decode>" if re.search(r"k_frames\w*<true", name) else "k_frames<encode>"
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
