@@ -31,6 +31,10 @@ def pick(acc, pat, counter):
 
 
 valu = json.load(open(f"{root}/pmcv/summary.json"))
+try:
+    stall = json.load(open(f"{root}/pmcs/summary.json"))
+except FileNotFoundError:
+    stall = {}
 fetch, write = per_kernel(f"{root}/pmct/fetch"), per_kernel(f"{root}/pmct/write")
 fcal, wcal = per_kernel(f"{root}/pmct/fetch_cal"), per_kernel(f"{root}/pmct/write_cal")
 cal_f, _ = pick(fcal, r"k_copy<false, 1>", "FETCH_SIZE")
@@ -53,6 +57,14 @@ for dec in (True, False):
     vv = {"kernel": kshort, "valu_wave_instr_per_launch": v["SQ_INSTS_VALU"], "salu_instr_per_launch": v["SQ_INSTS_SALU"],
           "vmem_instr_per_launch": v["SQ_INSTS_VMEM"], "waves": v["SQ_WAVES"],
           "valu_lane_ops_per_frame": v["SQ_INSTS_VALU"] * 64 / N}
+    st = stall.get("k_frames<%s>" % tag)
+    if st:  # quad-cycle counters, summed over the launch's waves; shares of the waves' lifetime
+        wc = st["SQ_WAVE_CYCLES"]
+        vv["wave_cycle_shares"] = {
+            "issuing (SQ_ACTIVE_INST_ANY)": st["SQ_ACTIVE_INST_ANY"] / wc,
+            "of which VALU (SQ_ACTIVE_INST_VALU)": st["SQ_ACTIVE_INST_VALU"] / wc,
+            "waiting at s_waitcnt / barriers (SQ_WAIT_ANY)": st["SQ_WAIT_ANY"] / wc,
+            "stalled at issue (SQ_WAIT_INST_ANY)": st["SQ_WAIT_INST_ANY"] / wc}
     if dec:
         out_t.update(t)
         out_v.update(vv)
