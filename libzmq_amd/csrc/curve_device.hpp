@@ -501,6 +501,62 @@ __device__ __forceinline__ void store_window(uint8_t *p, int nv, const uint32_t 
     }
 }
 
+// Store bytes w[0 .. NV) (NV a multiple of 4, 8 <= NV <= 64) at p, any
+// alignment, as one fixed sequence: the leading bytes up to the first 4-byte
+// boundary (a byte and a short store, each when needed), the aligned dwords
+// (dwordx4 where whole), the trailing bytes (a short and a byte store).  A
+// lane's stores each touch other lines than its neighbours' (frames sit at
+// arbitrary strides), so every store instruction costs the address unit all
+// 64 lanes; store_window's runtime length issues one instruction per dword
+// and per edge byte (about 22 for 16 bytes), this about 7 for 16 and 10 for
+// 64.
+template <int NV>
+__device__ __forceinline__ void store_bytes_c(uint8_t *p, const uint32_t w[16])
+{
+    static_assert(NV % 4 == 0 && NV >= 8 && NV <= 64, "whole dwords, at most one window");
+    typedef __attribute__((address_space(1))) uint8_t GU8_;
+    typedef __attribute__((address_space(1))) uint16_t GU16_;
+    typedef __attribute__((address_space(1))) uint32_t GU32_;
+    typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+    typedef unsigned int u32x3_ __attribute__((ext_vector_type(3)));
+    typedef __attribute__((address_space(1))) u32x2_ __attribute__((aligned(4))) GU2a4_;
+    typedef __attribute__((address_space(1))) u32x3_ __attribute__((aligned(4))) GU3a4_;
+    typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) u32x4_ __attribute__((aligned(4))) GU4a4_;
+    const uint64_t a = (uint64_t) (uintptr_t) p;
+    const uint32_t sh = (uint32_t) a & 3u, s = (4u - sh) & 3u; // s leading bytes before the first aligned dword
+    constexpr int ND = NV / 4;
+    uint32_t e[ND]; // e[k] = bytes [s + 4k, s + 4k + 4) of the stream w
+#pragma unroll
+    for (int k = 0; k < ND; ++k)
+        e[k] = __builtin_amdgcn_alignbyte(k + 1 < 16 ? w[k + 1] : 0u, w[k], s);
+    // leading bytes: s = 1 -> [0]; 2 -> [0,1]; 3 -> [0] and [1,2]
+    if (s & 1u)
+        *(GU8_ *) (uintptr_t) a = (uint8_t) w[0];
+    if (s & 2u)
+        *(GU16_ *) (uintptr_t) (a + (s & 1u)) = (uint16_t) (w[0] >> (8u * (s & 1u)));
+    // ND - 1 dwords for every alignment, the last one only when s == 0
+    const uint64_t q = a + s;
+    constexpr int NU = ND - 1;
+#pragma unroll
+    for (int g = 0; g + 4 <= NU; g += 4)
+        *(GU4a4_ *) (uintptr_t) (q + 4u * g) = (u32x4_){e[g], e[g + 1], e[g + 2], e[g + 3]};
+    constexpr int G4 = NU / 4 * 4;
+    if (NU - G4 == 3)
+        *(GU3a4_ *) (uintptr_t) (q + 4u * G4) = (u32x3_){e[G4], e[G4 + 1], e[G4 + 2]};
+    else if (NU - G4 == 2)
+        *(GU2a4_ *) (uintptr_t) (q + 4u * G4) = (u32x2_){e[G4], e[G4 + 1]};
+    else if (NU - G4 == 1)
+        *(GU32_ *) (uintptr_t) (q + 4u * G4) = e[G4];
+    if (s == 0u)
+        *(GU32_ *) (uintptr_t) (q + 4u * NU) = e[NU];
+    // trailing bytes (sh of them, the first bytes of e[NU]): 1 -> [0]; 2 -> [0,1]; 3 -> [0,1] and [2]
+    const uint64_t t = q + 4u * NU;
+    if (sh & 2u)
+        *(GU16_ *) (uintptr_t) t = (uint16_t) e[NU];
+    if (sh & 1u)
+        *(GU8_ *) (uintptr_t) (t + (sh & 2u)) = (uint8_t) (e[NU] >> (8u * (sh & 2u)));
+}
 
 // Zero bytes [p, p + len) by one lane: byte stores up to the first 16-byte
 // boundary and after the last, dwordx4 stores between.  (Only for regions a

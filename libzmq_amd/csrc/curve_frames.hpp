@@ -867,7 +867,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
 #pragma unroll
                 for (int k = 4; k < 16; ++k)
                     o[k] = 0;
-                store_window(dst, 16, o);
+                store_bytes_c<16>(dst, o);
                 const int nc = (int) (S < 64u ? S : 64u) - 32;
                 uint32_t ct[16];
 #pragma unroll
@@ -962,7 +962,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     poly_finish(fe_from_wide(wide), spad, tag);
     if (!DEC) {
         uint32_t o[16] = {tag[0], tag[1], tag[2], tag[3]};
-        store_window(dst + 16, 16, o);
+        store_bytes_c<16>(dst + 16, o);
     } else {
         if (lb && !(vn > excl))
             status = ZMQG_ERR_INVALID_SEQUENCE; // src/curve_mechanism_base.cpp:99-104 (before the MAC)
@@ -1220,6 +1220,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     // per window.
     const bool al64 = ZMQG_SEQ_AL64 && DEC && __builtin_amdgcn_ballot_w64(((uint32_t) (uintptr_t) dst & 63u) != 0u) == 0;
     uint32_t yp[16]; // al64: the previous window's output words
+    uint32_t ct0[8]; // encode: window 0's ciphertext words (stored with the tag)
 
     SEQ_STAMP(1u);
     // ---- step 0: window 0 (Poly1305 key, first 32 ciphertext bytes, header)
@@ -1291,20 +1292,25 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
                 if (!al64 || nw == 1u) // (al64: chunk 0 goes out with window 1)
                     store_window(dst, (int) (S < 64u ? S : 64u) - 33, pay);
             } else {
-                uint32_t o[16];
-                o[0] = 0x53454d07u; // "\x07MESSAGE" || nonce
-                o[1] = 0x45474153u;
-                o[2] = n0;
-                o[3] = n1;
 #pragma unroll
-                for (int k = 4; k < 16; ++k)
-                    o[k] = 0;
-                store_window(dst, 16, o);
-                uint32_t ct[16];
+                for (int k = 0; k < 8; ++k)
+                    ct0[k] = y[8 + k];
+                if (S < 64u) { // (a whole first window leaves at the end, with the tag)
+                    uint32_t o[16];
+                    o[0] = 0x53454d07u; // "\x07MESSAGE" || nonce
+                    o[1] = 0x45474153u;
+                    o[2] = n0;
+                    o[3] = n1;
 #pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    ct[k] = k < 8 ? y[8 + k] : 0u;
-                store_window(dst + 32, (int) (S < 64u ? S : 64u) - 32, ct);
+                    for (int k = 4; k < 16; ++k)
+                        o[k] = 0;
+                    store_bytes_c<16>(dst, o);
+                    uint32_t ct[16];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k)
+                        ct[k] = k < 8 ? y[8 + k] : 0u;
+                    store_window(dst + 32, (int) S - 32, ct);
+                }
             }
         }
     }
@@ -1523,8 +1529,17 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
     uint32_t tag[4];
     poly32_finish(h, spad, tag);
     if (!DEC) {
-        uint32_t o[16] = {tag[0], tag[1], tag[2], tag[3]};
-        store_window(dst + 16, 16, o);
+        if (S >= 64u) {
+            // wire bytes 0..63: "\x07MESSAGE", nonce, tag, the first 32
+            // ciphertext bytes -- one fixed store sequence at the frame's
+            // alignment instead of three byte-exact ones
+            const uint32_t o[16] = {0x53454d07u, 0x45474153u, n0,     n1,     tag[0], tag[1], tag[2], tag[3],
+                                    ct0[0],      ct0[1],      ct0[2], ct0[3], ct0[4], ct0[5], ct0[6], ct0[7]};
+            store_bytes_c<64>(dst, o);
+        } else {
+            const uint32_t o[16] = {tag[0], tag[1], tag[2], tag[3]};
+            store_bytes_c<16>(dst + 16, o);
+        }
     } else {
         if (lb && !(vn > excl))
             status = ZMQG_ERR_INVALID_SEQUENCE; // src/curve_mechanism_base.cpp:99-104 (before the MAC)

@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     if (!DEC) {
         // "\x07MESSAGE" || nonce || tag: wire bytes 0..31 (the rest went out cooperatively)
         uint32_t o[16] = {0x53454d07u, 0x45474153u, n0, n1, tag[0], tag[1], tag[2], tag[3]};
-        store_window(dst, 32, o);
+        store_bytes_c<32>(dst, o);
     } else {
         if (lb && !(vn > excl))
             status = ZMQG_ERR_INVALID_SEQUENCE; // src/curve_mechanism_base.cpp:99-104 (before the MAC)
