@@ -459,10 +459,11 @@ __device__ __forceinline__ void store_window(uint8_t *p, int nv, const uint32_t 
     const uintptr_t a = (uintptr_t) p;
     const uint32_t sh = (uint32_t) (a & 3);
     if (sh == 0 && nv >= 64) {
-        uint32_t *q = (uint32_t *) p;
+        typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) u32x4_ __attribute__((aligned(4))) GU4a4_;
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-            q[i] = w[i];
+        for (int i = 0; i < 4; ++i)
+            *(GU4a4_ *) (a + 16u * i) = (u32x4_){w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
         return;
     }
     const uint32_t s = (4u - sh) & 3u; // bytes before the first aligned dword
@@ -556,6 +557,52 @@ __device__ __forceinline__ void store_bytes_c(uint8_t *p, const uint32_t w[16])
         *(GU16_ *) (uintptr_t) t = (uint16_t) e[NU];
     if (sh & 1u)
         *(GU8_ *) (uintptr_t) (t + (sh & 2u)) = (uint8_t) (e[NU] >> (8u * (sh & 2u)));
+}
+
+// Store bytes [0, nb) of the word stream o (0 <= nb <= 68) at the 4-byte
+// aligned address a, as a fixed sequence of lane-predicated stores: four
+// dwordx4 (each while whole), three dwords, a short and a byte -- at most 9
+// instructions, where a per-word loop issues one per word (frame tails).
+__device__ __forceinline__ void store_tail(uint64_t a, uint32_t nb, const uint32_t o[17])
+{
+    typedef __attribute__((address_space(1))) uint8_t GU8_;
+    typedef __attribute__((address_space(1))) uint16_t GU16_;
+    typedef __attribute__((address_space(1))) uint32_t GU32_;
+    typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) u32x4_ __attribute__((aligned(4))) GU4a4_;
+    const uint32_t nw = nb >> 2, ng = nw >> 2; // whole words, whole 4-word groups
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g)
+        if (g < ng)
+            *(GU4a4_ *) (uintptr_t) (a + 16u * g) = (u32x4_){o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
+    // words 4ng .. nw-1 (at most 3; with ng = 4 only word 16), then the partial word nw
+    uint32_t r[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < 5; ++g)
+            if (g == ng && 4 * g + k < 17)
+                v = o[4 * g + k];
+        r[k] = v;
+    }
+    const uint64_t b = a + 16u * ng;
+    const uint32_t nr = nw - 4u * ng; // 0..3
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k)
+        if (k < nr)
+            *(GU32_ *) (uintptr_t) (b + 4u * k) = r[k];
+    uint32_t last = r[0];
+#pragma unroll
+    for (uint32_t k = 1; k < 4; ++k)
+        if (k == nr)
+            last = r[k];
+    const uint32_t tb = nb & 3u;
+    const uint64_t c = b + 4u * nr;
+    if (tb & 2u)
+        *(GU16_ *) (uintptr_t) c = (uint16_t) last;
+    if (tb & 1u)
+        *(GU8_ *) (uintptr_t) (c + (tb & 2u)) = (uint8_t) (last >> (8u * (tb & 2u)));
 }
 
 // Zero bytes [p, p + len) by one lane: byte stores up to the first 16-byte

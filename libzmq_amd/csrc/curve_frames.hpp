@@ -212,20 +212,8 @@ __device__ __forceinline__ void frame_store(uint64_t B, uint32_t w, uint32_t S, 
             }
         }
     } else {
-#pragma unroll
-        for (int k = 0; k < 17; ++k) {
-            const int s0 = (int) (64u * w + 4u * k) - (int) up; // stream byte of this word's byte 0
-            GU8 *t = (GU8 *) (uintptr_t) (a + 4u * k);
-            if (s0 + 4 <= (int) S) {
-                *(GU32 *) t = o[k];
-            } else if (s0 < (int) S) {
-                const int nb = (int) S - s0;
-#pragma unroll
-                for (int b = 0; b < 3; ++b)
-                    if (b < nb)
-                        t[b] = (uint8_t) (o[k] >> (8 * b));
-            }
-        }
+        // the frame's last window: stream bytes [64w - up, S), at most 68
+        store_tail(a, S + up - 64u * w, o);
     }
 }
 
@@ -1447,18 +1435,20 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
                 const uint32_t P = S - 33u; // (act: S >= 64t + 1 > 33)
                 if (act) {
                     const uint32_t r = P - 64u * (t - 1u);
-                    store_window(cdst, (int) (r < 64u ? r : 64u), o);
+                    const uint32_t o17[17] = {o[0], o[1], o[2],  o[3],  o[4],  o[5],  o[6],  o[7], o[8],
+                                              o[9], o[10], o[11], o[12], o[13], o[14], o[15], 0u};
+                    store_tail((uint64_t) (uintptr_t) cdst, r < 64u ? r : 64u, o17);
                 }
                 if (lastw && P > 64u * t) {
-                    uint32_t o2[16];
+                    uint32_t o2[17];
 #pragma unroll
                     for (int k = 0; k < 7; ++k)
                         o2[k] = __builtin_amdgcn_alignbyte(y[9 + k], y[8 + k], 1);
                     o2[7] = __builtin_amdgcn_alignbyte(0u, y[15], 1);
 #pragma unroll
-                    for (int k = 8; k < 16; ++k)
+                    for (int k = 8; k < 17; ++k)
                         o2[k] = 0;
-                    store_window(cdst + 64, (int) (P - 64u * t), o2);
+                    store_tail((uint64_t) (uintptr_t) (cdst + 64), P - 64u * t, o2);
                 }
             }
 #pragma unroll
