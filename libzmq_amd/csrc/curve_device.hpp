@@ -559,6 +559,37 @@ __device__ __forceinline__ void store_bytes_c(uint8_t *p, const uint32_t w[16])
         *(GU8_ *) (uintptr_t) (t + (sh & 2u)) = (uint8_t) (e[NU] >> (8u * (sh & 2u)));
 }
 
+// Load bytes p[0 .. NV) (NV a multiple of 16, at most 48; any alignment) as
+// NV/4 little-endian words: the aligned words covering them, NV/16 dwordx4
+// and one dword when p is not 4-byte aligned (a word holding a byte of the
+// range never crosses into a page the range does not touch) -- a fixed
+// sequence where load_window's runtime length issues one load per word.
+template <int NV>
+__device__ __forceinline__ void load_bytes_c(const uint8_t *p, uint32_t w[NV / 4])
+{
+    static_assert(NV % 16 == 0 && NV >= 16 && NV <= 48, "whole granules");
+    typedef __attribute__((address_space(1))) const uint32_t GCU32_;
+    typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const u32x4_ __attribute__((aligned(4))) GCU4a4_;
+    const uint64_t a = (uint64_t) (uintptr_t) p;
+    const uint32_t sh = (uint32_t) a & 3u;
+    const uint64_t q = a - sh;
+    constexpr int ND = NV / 4;
+    uint32_t d[ND + 1];
+#pragma unroll
+    for (int g = 0; g < ND / 4; ++g) {
+        const u32x4_ t = *(GCU4a4_ *) (uintptr_t) (q + 16u * g);
+        d[4 * g] = t.x;
+        d[4 * g + 1] = t.y;
+        d[4 * g + 2] = t.z;
+        d[4 * g + 3] = t.w;
+    }
+    d[ND] = sh ? *(GCU32_ *) (uintptr_t) (q + 4u * ND) : 0u;
+#pragma unroll
+    for (int k = 0; k < ND; ++k)
+        w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+}
+
 // Store bytes [0, nb) of the word stream o (0 <= nb <= 68) at the 4-byte
 // aligned address a, as a fixed sequence of lane-predicated stores: four
 // dwordx4 (each while whole), three dwords, a short and a byte -- at most 9

@@ -146,7 +146,14 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         S = sid_ok && !over ? 32u + hl + L_in : 0u;
         A = (uint64_t) (uintptr_t) src - 32u - hl;
         B = (uint64_t) (uintptr_t) dst;
-        load_window(src, L_in < 32u ? (int) L_in : 32, x0);
+        if (L_in >= 32u) { // payload bytes 0..31: two dwordx4 (and a dword when unaligned)
+            load_bytes_c<32>(src, x0);
+#pragma unroll
+            for (int k = 8; k < 16; ++k)
+                x0[k] = 0;
+        } else {
+            load_window(src, (int) L_in, x0);
+        }
     } else {
         // the wire frame's first window: header, nonce, tag, 32 ciphertext bytes
         A = (uint64_t) (uintptr_t) src;
