@@ -61,22 +61,36 @@ typedef u32x4 u32x4_u1 __attribute__((aligned(1)));
 typedef __attribute__((address_space(3))) void StLdsVoid;
 typedef __attribute__((address_space(1))) void StGVoid;
 
-// bytes [lo, hi) (0 <= lo < hi <= 16) of granule v at the 16-byte aligned address a
+// bytes [lo, hi) (0 <= lo < hi <= 16) of granule v at the 16-byte aligned
+// address a: the bytes before the first whole word (up to 3), the whole
+// words (up to 4), the bytes after the last (up to 3) -- ten lane-predicated
+// stores at most (a frame's edge granules; the per-byte form issued twenty).
 __device__ __forceinline__ void granule_store_part(uint64_t a, uint32_t lo, uint32_t hi, const u32x4 &v)
 {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t fa = (lo + 3u) >> 2, la = hi >> 2; // whole words [fa, la)
+    const uint32_t le = (4u * fa < hi ? 4u * fa : hi); // leading bytes [lo, le)
+    uint32_t wl = w[0], wt = w[0];                      // the words holding them / the trailing bytes
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t b0 = 4 * q;
-        if (lo <= b0 && b0 + 4 <= hi) {
-            *(GU32 *) (uintptr_t) (a + b0) = w[q];
-        } else {
-#pragma unroll
-            for (uint32_t b = 0; b < 4; ++b)
-                if (b0 + b >= lo && b0 + b < hi)
-                    *(GU8 *) (uintptr_t) (a + b0 + b) = (uint8_t) (w[q] >> (8 * b));
-        }
+    for (uint32_t q = 1; q < 4; ++q) {
+        if (q == (lo >> 2))
+            wl = w[q];
+        if (q == la)
+            wt = w[q];
     }
+#pragma unroll
+    for (uint32_t b = 0; b < 3; ++b)
+        if (lo + b < le)
+            *(GU8 *) (uintptr_t) (a + lo + b) = (uint8_t) (wl >> (8u * ((lo + b) & 3u)));
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q)
+        if (q >= fa && q < la)
+            *(GU32 *) (uintptr_t) (a + 4u * q) = w[q];
+    const uint32_t ts = 4u * la > le ? 4u * la : le; // trailing bytes [ts, hi), inside word la
+#pragma unroll
+    for (uint32_t b = 0; b < 3; ++b)
+        if (ts + b < hi && la < 4u)
+            *(GU8 *) (uintptr_t) (a + ts + b) = (uint8_t) (wt >> (8u * ((ts + b) & 3u)));
 }
 
 // One LDS-DMA granule per lane: global [gaddr, +16) -> LDS lds_base + 16 * lane
