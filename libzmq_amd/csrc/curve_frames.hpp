@@ -1102,15 +1102,19 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             B = (uint64_t) (uintptr_t) dst - 33u;
         }
     };
-    if (threadIdx.x == 0) { // the call state (see call_state_begin)
-        CallState c;
-        c.epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        c.ticket = use_ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
-        c.nbase = DEC ? 0ull : nonce_base(ctl);
-        sh_cs = c;
+    // the call state (see call_state_begin): thread 0's reads go out first,
+    // the frame's loads behind them, and the reads are waited for (to publish
+    // them in LDS) only after both are in flight
+    CallState c0{};
+    if (threadIdx.x == 0) {
+        c0.epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c0.ticket = use_ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
+        c0.nbase = DEC ? 0ull : nonce_base(ctl);
     }
     if (!use_ticket)
         fetch(blockIdx.x);
+    if (threadIdx.x == 0)
+        sh_cs = c0;
     __syncthreads();
     const CallState cs = sh_cs;
     const uint32_t epoch = cs.epoch;
