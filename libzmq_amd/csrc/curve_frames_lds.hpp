@@ -513,7 +513,11 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         const unsigned long long P = lookback_excl(wg, epoch, rp.lb_flag, rp.lb_agg, rp.lb_inc);
         if (threadIdx.x == 0) {
             const unsigned long long inc = P > wagg ? P : wagg;
-            lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
+            // (a grid of at most kFramesBS workgroups looks back over every
+            // aggregate in one round and needs no inclusive values: no
+            // publish, and no drain of this wave's last stores for it)
+            if (gridDim.x > kFramesBS)
+                lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
             if (wg + 1 == gridDim.x) {
                 *rp.peer = inc > psn ? inc : psn;
                 if (rp.smax)
