@@ -58,11 +58,38 @@ def parse():
     p.add_argument("--configs", default="3,4,5", help="which of the other BASELINE configs to measure")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from the host instead of replaying the captured K steps as one hipGraph")
+    p.add_argument("--dry-run", action="store_true",
+                   help="start the ranks, meet at one barrier, print one JSON line per rank and exit before any "
+                        "GPU call (tests the multi-GPU launch on a CPU host)")
     return p.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` outside torchrun: start N ranks, one process
+    per GPU, as a FRESH child `torch.distributed.run` (this process has made
+    no GPU call, and it does not exec: it waits for the child and exits with
+    its return code).  Rank 0's JSON line reaches our stdout through the
+    inherited descriptors."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
 
@@ -71,6 +98,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.gpus != world:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}; reporting n_gpus = {world}", file=sys.stderr)
+    if args.dry_run:
+        if world > 1:
+            dist.barrier()
+        print(json.dumps({"dry_run": True, "rank": rank, "local_rank": local, "world": world}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # one process per GPU; (a rehearsal with more ranks than GPUs shares them)
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
@@ -415,6 +451,8 @@ def host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_o
     out["zerocopy_pinned"] = {"value": 4 * n * P / 2**30 / (t1 - t0), "unit": "GiB/s",
                               "note": "encode+decode, kernels on pinned host memory over PCIe"}
 
+    out["pinned_dma"] = pinned_dma(C, torch, dev, local, hp, precom, flags, flags_np, n, P, W)
+
     hpn = hp.numpy()
     hin = np.arange(n, dtype=np.uint64) * P
     hout = np.arange(n, dtype=np.uint64) * W
@@ -436,6 +474,94 @@ def host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_o
     out["pageable_staged"] = {"value": reps * n * P / 2**30 / (t1 - t0), "unit": "GiB/s",
                               "note": "zmqg_encode_host + zmqg_decode_host, pageable buffers, H2D+D2H included"}
     return out
+
+
+def pinned_dma(C, torch, dev, local, hp, precom, flags, flags_np, n, P, W, chunks=8, reps=4):
+    """The north_star's host-memory round trip through pinned hipMemcpyAsync:
+    payload and wire in pinned host buffers (the I/O thread's socket side),
+    the batch cut into `chunks` slices pipelined over three streams --
+      send path:    H2D payload slice -> encode -> D2H wire slice
+      receive path: H2D wire slice (the bytes just sent) -> decode -> D2H payload
+    -- so copies of one slice overlap the kernels and copies of the others
+    (copy streams per direction; device buffers per slice).  Every byte
+    crosses PCIe four times per round trip (P + W each way), as in the
+    zero-copy form.  Payload GiB/s of round trips, whole batch checked."""
+    m = n // chunks
+    assert m * chunks == n
+    i64 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    enc = C.CurveContext(local, 1)
+    enc.session_set(0, precom, C.CLIENT_PREFIX, C.SERVER_PREFIX)
+    enc.set_nonce(0, 3)
+    dec = C.CurveContext(local, 1)
+    dec.session_set(0, precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+    sid = i32(np.zeros(m, np.uint32))
+    in_off = i64(np.arange(m, dtype=np.uint64) * P)
+    out_off = i64(np.arange(m, dtype=np.uint64) * W)
+    lens = i32(np.full(m, P, np.uint32))
+    wlen = i32(np.full(m, W, np.uint32))
+    wire_h = torch.zeros(n * W, dtype=torch.uint8).pin_memory()
+    back_h = torch.zeros(n * P, dtype=torch.uint8).pin_memory()
+    d_pay = [torch.empty(m * P, dtype=torch.uint8, device=dev) for _ in range(chunks)]
+    d_wire = [torch.empty(m * W, dtype=torch.uint8, device=dev) for _ in range(chunks)]
+    d_wire2 = [torch.empty(m * W, dtype=torch.uint8, device=dev) for _ in range(chunks)]
+    d_back = [torch.empty(m * P, dtype=torch.uint8, device=dev) for _ in range(chunks)]
+    fl = [torch.empty(m, dtype=torch.uint8, device=dev) for _ in range(chunks)]
+    st = [torch.empty(m, dtype=torch.int32, device=dev) for _ in range(chunks)]
+    fls = [flags[c * m:(c + 1) * m] for c in range(chunks)]
+    h2d, comp, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    ev = lambda: torch.cuda.Event()
+
+    def one():
+        # slice k's send stages, then slice k-1's receive stages: each stream
+        # runs its work in slice order and waits only on the slice it needs
+        sent = [None] * chunks
+        h2d.wait_stream(comp)  # the previous round trip's readers of the slice buffers are done
+        h2d.wait_stream(d2h)
+        for k in range(chunks + 1):
+            if k < chunks:
+                c = k
+                with torch.cuda.stream(h2d):
+                    d_pay[c].copy_(hp[c * m * P:(c + 1) * m * P], non_blocking=True)
+                    a = ev()
+                    a.record(h2d)
+                comp.wait_event(a)
+                enc.encode_batch(sid, None, fls[c], in_off, lens, d_pay[c], out_off, d_wire[c], comp, max_len=P,
+                                 nonce_auto=True)
+                b = ev()
+                b.record(comp)
+                d2h.wait_event(b)
+                with torch.cuda.stream(d2h):
+                    wire_h[c * m * W:(c + 1) * m * W].copy_(d_wire[c], non_blocking=True)
+                    sent[c] = ev()
+                    sent[c].record(d2h)
+            if k >= 1:  # receive path: the wire as it left
+                c = k - 1
+                h2d.wait_event(sent[c])
+                with torch.cuda.stream(h2d):
+                    d_wire2[c].copy_(wire_h[c * m * W:(c + 1) * m * W], non_blocking=True)
+                    a = ev()
+                    a.record(h2d)
+                comp.wait_event(a)
+                dec.decode_batch(sid, out_off, wlen, d_wire2[c], in_off, d_back[c], fl[c], st[c], comp, max_len=W)
+                b = ev()
+                b.record(comp)
+                d2h.wait_event(b)
+                with torch.cuda.stream(d2h):
+                    back_h[c * m * P:(c + 1) * m * P].copy_(d_back[c], non_blocking=True)
+
+    one()  # untimed: first touch
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    assert all(int((s != 0).sum()) == 0 for s in st) and torch.equal(back_h, hp), "pinned DMA round trip"
+    return {"value": reps * n * P / 2**30 / (t1 - t0), "unit": "GiB/s",
+            "note": f"encode+decode round trip, pinned host buffers, hipMemcpyAsync H2D/D2H on two copy streams "
+                    f"overlapped with the kernels in {chunks} slices (P + W bytes each way per message)"}
 
 
 def host_cores():

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define ZMQG_CURVE_ABI_VERSION 3
+#define ZMQG_CURVE_ABI_VERSION 4
 
 /* Per-frame status codes, identical to include/zmq.h:424-437. */
 #define ZMQG_STATUS_OK 0
@@ -147,11 +147,13 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  * the reference's check_validity does (src/curve_mechanism_base.cpp:98-106,
  * including on a later MAC failure).
  *
- * In-place decode: `out` may be `in`, with every frame in one of the two
- * layouts the reference produces (src/curve_mechanism_base.cpp:222-260):
- * out_off[i] = in_off[i] + 33, the payload where crypto_box_open_easy_afternm
- * leaves it, or out_off[i] = in_off[i], the payload at the frame's start as
- * after the reference's memmove.  Otherwise `out` must not overlap `in`.  On
+ * In-place decode: `out` may be `in`, with every frame in one of two
+ * layouts: out_off[i] = in_off[i] + 33, each payload byte over its own
+ * ciphertext byte (the reference's crypto_box_open_easy_afternm decrypts
+ * into message + 16, src/curve_mechanism_base.cpp:222-228, which puts the
+ * flags byte at wire offset 16 and the payload at 17 -- a different layout,
+ * not offered here), or out_off[i] = in_off[i], the payload at the frame's
+ * start as after the reference's memmove (:253-260).  Otherwise `out` must not overlap `in`.  On
  * failure the payload region is zero-filled as above; in the second layout a
  * frame of more than 4.5 KiB that fails has its whole wire region zeroed.
  *
@@ -161,7 +163,9 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  * reference's libsodium verifies first and writes nothing for a forged frame
  * (SURVEY.md a12).  Results at completion are identical; a caller whose
  * `out` is visible to another party while the call runs (e.g. mapped host
- * memory read by a second thread) must not read it before completion. */
+ * memory read by a second thread) sets ZMQG_OPT_VERIFY_FIRST
+ * (zmqg_decode_batch_ex), under which `out` only ever receives verified
+ * payloads and zeros. */
 int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
                       const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
                       uint8_t *flags_out, int32_t *status_out, void *stream);
@@ -189,14 +193,32 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  *                    per session, the largest header-valid nonce among this
  *                    batch's frames (0 where it has none) -- the value a rank
  *                    contributes to shard.peer_prefix when a session's frames
- *                    span GPUs. */
+ *                    span GPUs.
+ *   flags            ZMQG_OPT_VERIFY_FIRST (decode): no byte of `out` is
+ *                    written before the frame's tag and replay verdict, as
+ *                    libsodium's open verifies before it decrypts
+ *                    (src/curve_mechanism_base.cpp:226-228).  The frames are
+ *                    decoded into a device staging area of the ctx laid out
+ *                    like `out`, then one kernel copies each verified payload
+ *                    to out[out_off[i]] and zero-fills the payload region of
+ *                    each failed one (a frame above max_len, or shorter than
+ *                    33 bytes, is left as it was).  Needs out_bytes.  For
+ *                    `out` another party can read while the call runs (mapped
+ *                    host memory: curve_batcher_t's receive slots).  Costs one
+ *                    extra read and write of the payload bytes.
+ *   out_bytes        extent of `out`: every out_off[i] + wire_len[i] - 33 is
+ *                    at most this (required by ZMQG_OPT_VERIFY_FIRST).
+ * A caller built against the struct without out_bytes passes the smaller
+ * size and gets the old behaviour. */
 #define ZMQG_OPT_NONCE_AUTO 1u
+#define ZMQG_OPT_VERIFY_FIRST 2u
 typedef struct zmqg_batch_opts {
     uint32_t size;
     uint32_t flags;
     uint64_t max_len;
     int32_t *status_out;
     uint64_t *session_max_out;
+    uint64_t out_bytes;
 } zmqg_batch_opts;
 int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
                          const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,

@@ -149,6 +149,8 @@ struct Workspace {
     unsigned long long *rt = nullptr; // replay tables: [tiles][S] then [row blocks][S] (also the nonce tables)
     uint64_t *nonce = nullptr;        // [cap] ZMQG_OPT_NONCE_AUTO over several sessions: each frame's nonce
     size_t rt_cap = 0;
+    uint8_t *stage = nullptr;         // ZMQG_OPT_VERIFY_FIRST: decoded payloads before the verdict copy
+    size_t stage_cap = 0;
     bool use_last = false; // the last replay ran the sort fallback (k_fixup writes the peer nonces)
 };
 
@@ -898,11 +900,15 @@ __global__ __launch_bounds__(256) void k_nonce_tiles(uint32_t n, uint32_t T, uin
 
 __global__ __launch_bounds__(256) void k_nonce_colblk(uint32_t tiles, uint32_t S,
                                                      const unsigned long long *__restrict__ tab,
-                                                     unsigned long long *__restrict__ blk)
+                                                     unsigned long long *__restrict__ blk,
+                                                     const unsigned long long *__restrict__ send,
+                                                     unsigned long long *__restrict__ snap)
 {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x, rb = blockIdx.y;
     if (s >= S)
         return;
+    if (rb == 0) // the send counters as they were before this call, for k_nonce_colscan
+        snap[s] = send[s];
     const uint32_t r0 = rb * kReplayRB, r1 = r0 + kReplayRB < tiles ? r0 + kReplayRB : tiles;
     unsigned long long m = 0;
     for (uint32_t r = r0; r < r1; ++r)
@@ -912,12 +918,16 @@ __global__ __launch_bounds__(256) void k_nonce_colblk(uint32_t tiles, uint32_t S
 
 __global__ __launch_bounds__(256) void k_nonce_colscan(uint32_t tiles, uint32_t S, unsigned long long *__restrict__ tab,
                                                       const unsigned long long *__restrict__ blk,
+                                                      const unsigned long long *__restrict__ snap,
                                                       unsigned long long *__restrict__ send)
 {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x, rb = blockIdx.y;
     if (s >= S)
         return;
-    unsigned long long m = send[s];
+    // the base comes from the snapshot k_nonce_colblk took: the last row
+    // block advances send[s] below, and nothing orders that store against
+    // the other row blocks of this launch
+    unsigned long long m = snap[s];
     for (uint32_t k = 0; k < rb; ++k)
         m += blk[(size_t) k * S + s];
     const uint32_t r0 = rb * kReplayRB, r1 = r0 + kReplayRB < tiles ? r0 + kReplayRB : tiles;
@@ -927,7 +937,7 @@ __global__ __launch_bounds__(256) void k_nonce_colscan(uint32_t tiles, uint32_t 
         *p = m;
         m += x;
     }
-    if (r1 == tiles) // every block has read send[s] above (k_nonce_frames runs after this kernel)
+    if (r1 == tiles) // (no block of this launch reads send[s])
         send[s] = m;
 }
 
@@ -1847,7 +1857,7 @@ int nonce_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st)
     while ((nn + T - 1) / T > kReplayMaxTiles)
         T *= 2;
     const uint32_t tiles = (nn + T - 1) / T, rbs = (tiles + kReplayRB - 1) / kReplayRB;
-    const size_t need = ((size_t) tiles + rbs) * S;
+    const size_t need = ((size_t) tiles + rbs + 1) * S; // tables, block sums, send snapshot
     if (need > w.rt_cap) {
         if (w.rt)
             ZCHECK(ctx, hipFreeAsync(w.rt, st));
@@ -1855,14 +1865,15 @@ int nonce_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st)
         ZCHECK(ctx, hipMallocAsync((void **) &w.rt, need * sizeof(unsigned long long), st));
         w.rt_cap = need;
     }
-    unsigned long long *tab = w.rt, *blk = w.rt + (size_t) tiles * S;
+    unsigned long long *tab = w.rt, *blk = w.rt + (size_t) tiles * S, *snap = blk + (size_t) rbs * S;
     hipLaunchKernelGGL(k_nonce_tiles, dim3(tiles), dim3(256), S * sizeof(uint32_t), st, nn, T, S, sid, tab);
     ZCHECK(ctx, hipGetLastError());
     const dim3 cg((S + 255) / 256, rbs);
-    hipLaunchKernelGGL(k_nonce_colblk, cg, dim3(256), 0, st, tiles, S, (const unsigned long long *) tab, blk);
+    hipLaunchKernelGGL(k_nonce_colblk, cg, dim3(256), 0, st, tiles, S, (const unsigned long long *) tab, blk,
+                       (const unsigned long long *) ctx->send, snap);
     ZCHECK(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_nonce_colscan, cg, dim3(256), 0, st, tiles, S, tab, (const unsigned long long *) blk,
-                       ctx->send);
+                       (const unsigned long long *) snap, ctx->send);
     ZCHECK(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_nonce_frames, dim3(tiles), dim3(64), S * sizeof(unsigned long long), st, nn, T, S, sid,
                        (const unsigned long long *) tab, w.nonce);
@@ -1883,7 +1894,7 @@ int replay_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st
         while ((nn + T - 1) / T > kReplayMaxTiles)
             T *= 2;
         const uint32_t tiles = (nn + T - 1) / T, rbs = (tiles + kReplayRB - 1) / kReplayRB;
-        const size_t need = ((size_t) tiles + rbs) * S;
+        const size_t need = ((size_t) tiles + rbs + 1) * S; // tables, block sums, send snapshot
         if (need > w.rt_cap) {
             if (w.rt)
                 ZCHECK(ctx, hipFreeAsync(w.rt, st));
@@ -2000,7 +2011,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     Workspace &w = ctx->ws;
     void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
                     w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.post, w.psnap, w.blockmax, w.zs,
-                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, w.rt, w.nonce, ctx->sessions, ctx->peer, ctx->send, ctx->dbuf};
+                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, w.rt, w.nonce, w.stage, ctx->sessions, ctx->peer, ctx->send, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
             (void) hipFree(p);
@@ -2172,9 +2183,49 @@ uint64_t zmqg_wire_size(uint8_t msg_flags, int downgrade_sub, uint64_t payload_l
     return 32 + hl + payload_len;
 }
 
+// opts of a caller built against the struct before out_bytes: the fields
+// it has are read, out_bytes is taken as 0
 static int check_opts(const zmqg_batch_opts *o)
 {
-    return o && o->size < sizeof(zmqg_batch_opts) ? -EINVAL : 0;
+    return o && o->size < offsetof(zmqg_batch_opts, out_bytes) ? -EINVAL : 0;
+}
+
+static uint64_t opt_out_bytes(const zmqg_batch_opts *o)
+{
+    return o && o->size >= sizeof(zmqg_batch_opts) ? o->out_bytes : 0;
+}
+
+// ZMQG_OPT_VERIFY_FIRST: frame i's payload, decoded into the staging area at
+// the same offset (and the same alignment mod 16) as in `out`, goes to `out`
+// once its status is known: the payload if the frame verified, zeros if it
+// failed; a frame the decode left as it was (above the bound, or shorter
+// than the 33-byte MESSAGE minimum) is left as it was here too.  One
+// workgroup per frame; 16-byte stores in the aligned middle.
+__global__ __launch_bounds__(256) void k_verify_copy(uint32_t n, const uint8_t *__restrict__ stage,
+                                                     uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off,
+                                                     const uint32_t *__restrict__ wire_len,
+                                                     const int32_t *__restrict__ status)
+{
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t wl = wire_len[i];
+        const int32_t stt = status[i];
+        if (wl <= 33u || stt == ZMQG_ERR_BOUND)
+            continue;
+        const uint64_t L = wl - 33u, o = out_off[i];
+        const bool ok = stt == 0;
+        const uint8_t *src = stage + o;
+        uint8_t *dst = out + o;
+        const uint64_t head = (16u - ((uintptr_t) dst & 15u)) & 15u;
+        const uint64_t h = head < L ? head : L;
+        const uint64_t body = (L - h) & ~15ull;
+        for (uint64_t k = threadIdx.x; k < h; k += blockDim.x)
+            dst[k] = ok ? src[k] : 0;
+        const u32x4 z = {0, 0, 0, 0};
+        for (uint64_t k = h + 16ull * threadIdx.x; k < h + body; k += 16ull * blockDim.x)
+            *(GU4 *) (uintptr_t) (dst + k) = ok ? *(const GCU4 *) (uintptr_t) (src + k) : z;
+        for (uint64_t k = h + body + threadIdx.x; k < L; k += blockDim.x)
+            dst[k] = ok ? src[k] : 0;
+    }
 }
 
 int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
@@ -2204,7 +2255,7 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         ctl.enc_status = opts->status_out;
         ctl.max_len = opts->max_len;
         // every frame within the bound fits the frame kernel: no body launch
-        ctl.no_body = opts->max_len && opts->max_len + 43u <= kMaxFrameStream;
+        ctl.no_body = opts->max_len && opts->max_len <= kMaxFrameStream - 43u; // (no wrap near UINT64_MAX)
     }
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
@@ -2255,6 +2306,10 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         return 0;
     if (!sid || !in_off || !wire_len || !in || !out_off || !out || !flags_out || !status_out)
         return -EINVAL;
+    const bool verify_first = opts && (opts->flags & ZMQG_OPT_VERIFY_FIRST);
+    const uint64_t out_bytes = opt_out_bytes(opts);
+    if (verify_first && out_bytes == 0)
+        return -EINVAL;
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
     ctx->last_stream = st;
@@ -2262,6 +2317,19 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     if (rc)
         return rc;
     Workspace &w = ctx->ws;
+    uint8_t *const out_user = out;
+    if (verify_first) {
+        // the staging area mirrors `out`: same offsets, same alignment mod 16
+        const size_t need = out_bytes + 16;
+        if (need > w.stage_cap) {
+            if (w.stage)
+                ZCHECK(ctx, hipFreeAsync(w.stage, st));
+            w.stage = nullptr;
+            ZCHECK(ctx, hipMallocAsync((void **) &w.stage, need, st));
+            w.stage_cap = need;
+        }
+        out = w.stage + ((uintptr_t) out_user & 15u);
+    }
     const uint32_t nn = (uint32_t) n;
     const int G = lanes_per_frame(ctx, nn);
     const bool multi = ctx->sort_bits > 0;
@@ -2319,6 +2387,12 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         hipLaunchKernelGGL(k_fixup, dim3((nn + kFixupThreads - 1) / kFixupThreads), dim3(kFixupThreads), 0, st, nn,
                            kMaxFrameStream, w.v, w.psnap, w.excl, w.use_last ? w.last : nullptr, sid,
                            ctx->max_sessions, wire_len, out_off, out, status_out, flags_out, ctx->peer, smax);
+        ZCHECK(ctx, hipGetLastError());
+    }
+    if (verify_first) {
+        const uint32_t g = nn < 65536u ? nn : 65536u;
+        hipLaunchKernelGGL(k_verify_copy, dim3(g), dim3(256), 0, st, nn, (const uint8_t *) out, out_user, out_off,
+                           wire_len, (const int32_t *) status_out);
         ZCHECK(ctx, hipGetLastError());
     }
     call.end();

@@ -63,11 +63,12 @@ _lib.zmqg_wire_size.restype = _U64
 _lib.zmqg_encode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
 OPT_NONCE_AUTO = 1  # zmqg_batch_opts.flags: encode nonces from the sessions' send counters
+OPT_VERIFY_FIRST = 2  # zmqg_batch_opts.flags: decode writes out only after each frame's verdict
 
 
 class BatchOpts(ctypes.Structure):  # zmqg_batch_opts
     _fields_ = [("size", _U32), ("flags", _U32), ("max_len", _U64), ("status_out", _P),
-                ("session_max_out", _P)]
+                ("session_max_out", _P), ("out_bytes", _U64)]
 
 
 _lib.zmqg_encode_batch_ex.argtypes = [_P, _U64] + [_P] * 8 + [ctypes.POINTER(BatchOpts), _P]
@@ -100,7 +101,7 @@ _lib.zmqg_ctx_set_profiling.argtypes = [_P, ctypes.c_int]
 _lib.zmqg_ctx_get_profile.argtypes = [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
 _lib.zmqg_last_error.argtypes = [_P]
 _lib.zmqg_last_error.restype = ctypes.c_char_p
-assert _lib.zmqg_abi_version() == 3
+assert _lib.zmqg_abi_version() == 4
 
 
 def lib():
@@ -207,11 +208,12 @@ class CurveContext:
     # max_len / status_out / session_max_out: zmqg_batch_opts (the _ex calls)
     # nonce_auto: encode takes nonces from the sessions' send counters (nonce may be None)
     @staticmethod
-    def _opts(max_len, status_out, session_max_out, nonce_auto=False):
-        if not max_len and status_out is None and session_max_out is None and not nonce_auto:
+    def _opts(max_len, status_out, session_max_out, nonce_auto=False, verify_first=False, out_bytes=0):
+        if not max_len and status_out is None and session_max_out is None and not nonce_auto and not verify_first:
             return None
-        o = BatchOpts(ctypes.sizeof(BatchOpts), OPT_NONCE_AUTO if nonce_auto else 0, int(max_len or 0),
-                      _ptr(status_out), _ptr(session_max_out))
+        fl = (OPT_NONCE_AUTO if nonce_auto else 0) | (OPT_VERIFY_FIRST if verify_first else 0)
+        o = BatchOpts(ctypes.sizeof(BatchOpts), fl, int(max_len or 0), _ptr(status_out), _ptr(session_max_out),
+                      int(out_bytes))
         return ctypes.byref(o), o
 
     def encode_batch(self, sid, nonce, flags, in_off, length, inp, out_off, out, stream=None, max_len=0,
@@ -223,11 +225,14 @@ class CurveContext:
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_encode_batch")
 
     def decode_batch(self, sid, in_off, wire_len, inp, out_off, out, flags_out, status_out, stream=None, max_len=0,
-                     session_max_out=None):
+                     session_max_out=None, verify_first=False):
         """session_max_out: int64 tensor of max_sessions entries (device),
-        receives each session's largest header-valid nonce of the batch."""
+        receives each session's largest header-valid nonce of the batch.
+        verify_first: ZMQG_OPT_VERIFY_FIRST (out receives only verified
+        payloads and zeros; out's extent is taken from the tensor)."""
         n = int(sid.numel())
-        o = self._opts(max_len, None, session_max_out)
+        o = self._opts(max_len, None, session_max_out, verify_first=verify_first,
+                       out_bytes=out.numel() * out.element_size() if verify_first else 0)
         self._check(_lib.zmqg_decode_batch_ex(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
                                               _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_decode_batch")

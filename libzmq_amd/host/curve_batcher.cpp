@@ -192,10 +192,10 @@ int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
         errno = EIO;
         return -1;
     }
-    //  decoded in place: the payload is left where crypto_box_open_easy_afternm
-    //  leaves it in the reference, at wire offset 33 of the frame
-    //  (src/curve_mechanism_base.cpp:222-228), so a decode slot needs no
-    //  output area
+    //  decoded in place: each payload byte is left over its own ciphertext
+    //  byte, at wire offset 33 of the frame, so a decode slot needs no output
+    //  area (the reference decrypts into message + 16 instead,
+    //  src/curve_mechanism_base.cpp:222-228, and then moves the payload)
     if (open_slot (decode_kind, size_, 0) != 0)
         return -1;
     slot_t *s = _open[decode_kind];
@@ -218,10 +218,19 @@ int curve_batcher_t::launch (slot_t *s)
         rc = zmqg_encode_batch (_ctx, s->n, s->sid, s->nonce, s->flags,
                                 s->in_off, s->len, s->in, s->out_off, s->out,
                                 _stream);
-    else
-        rc = zmqg_decode_batch (_ctx, s->n, s->sid, s->in_off, s->len, s->in,
-                                s->out_off, s->in, s->flags_out, s->status,
-                                _stream);
+    else {
+        //  the slot is host memory the I/O thread can read while the batch
+        //  runs: verify before any plaintext reaches it, as libsodium's open
+        //  does (src/curve_mechanism_base.cpp:226-228)
+        zmqg_batch_opts o;
+        memset (&o, 0, sizeof o);
+        o.size = sizeof o;
+        o.flags = _config.verify_first ? ZMQG_OPT_VERIFY_FIRST : 0;
+        o.out_bytes = s->in_used;
+        rc = zmqg_decode_batch_ex (_ctx, s->n, s->sid, s->in_off, s->len,
+                                   s->in, s->out_off, s->in, s->flags_out,
+                                   s->status, &o, _stream);
+    }
     if (rc == 0)
         rc = zmqg_fence_record (_ctx, _stream, &s->fence);
     if (rc != 0) {

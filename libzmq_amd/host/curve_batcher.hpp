@@ -26,8 +26,9 @@
 // only host copies are the submit copy (the engine's own copy into its send
 // or receive buffer in the reference) and whatever the sink does.  Decode
 // runs in place inside the slot's input area: each payload is left at wire
-// offset 33 of its frame, where the reference's crypto_box_open_easy_afternm
-// leaves it (src/curve_mechanism_base.cpp:222-228).  Slots
+// offset 33 of its frame, every byte over its own ciphertext byte (the
+// reference's crypto_box_open_easy_afternm decrypts into message + 16,
+// src/curve_mechanism_base.cpp:222-228, before its memmove).  Slots
 // cycle free -> open -> in flight -> free; when none is free, a submit
 // blocks on the oldest in-flight slot and delivers it (back-pressure).
 //
@@ -79,7 +80,13 @@ class curve_batcher_t
         size_t slot_msgs;  //  messages per slot
         size_t slot_bytes; //  input bytes per slot (payloads or wire frames)
         int slots;         //  slots in rotation (>= 2)
-        config_t () : slot_msgs (8192), slot_bytes (8u << 20), slots (4) {}
+        //  receive slots decoded with ZMQG_OPT_VERIFY_FIRST: the pinned slot
+        //  never holds plaintext of a frame that fails (default on)
+        bool verify_first;
+        config_t () :
+            slot_msgs (8192), slot_bytes (8u << 20), slots (4), verify_first (true)
+        {
+        }
     };
 
     //  All connections submitted must live on ctx_.  stream_: a hipStream_t

@@ -15,9 +15,9 @@ struct thread_state_t
 {
     zmqg_ctx *ctx;
     bool failed;
-    uint32_t next;
+    uint32_t next, limit;
     std::vector<uint32_t> free_sids;
-    thread_state_t () : ctx (NULL), failed (false), next (0) {}
+    thread_state_t () : ctx (NULL), failed (false), next (0), limit (0) {}
     ~thread_state_t ()
     {
         if (ctx)
@@ -27,12 +27,20 @@ struct thread_state_t
 thread_local thread_state_t tls_state;
 }
 
+uint32_t session_limit ()
+{
+    const char *e = getenv ("ZMQG_THREAD_SESSIONS");
+    const long v = e ? atol (e) : 0;
+    return v > 0 && v <= (1L << 24) ? (uint32_t) v : (uint32_t) thread_sessions;
+}
+
 zmqg_ctx *thread_ctx ()
 {
     thread_state_t &t = tls_state;
     if (!t.ctx && !t.failed) {
         const char *d = getenv ("ZMQG_DEVICE");
-        if (zmqg_ctx_create (d ? atoi (d) : 0, thread_sessions, &t.ctx) != 0) {
+        t.limit = session_limit ();
+        if (zmqg_ctx_create (d ? atoi (d) : 0, t.limit, &t.ctx) != 0) {
             t.ctx = NULL;
             t.failed = true;
         }
@@ -52,7 +60,7 @@ int acquire_session (uint32_t *sid_)
         t.free_sids.pop_back ();
         return 0;
     }
-    if (t.next == thread_sessions) {
+    if (t.next == t.limit) {
         errno = ENOMEM;
         return -1;
     }

@@ -52,9 +52,13 @@ struct msg_buf_t
 //  and so each curve_encoding_t, on one I/O thread for its whole life
 //  (src/io_thread.hpp); a zmqg_ctx is externally synchronised, so each I/O
 //  thread gets its own, created on first use on device ZMQG_DEVICE (default
-//  0) with thread_sessions slots.  acquire_session returns 0 and a free slot
-//  of the calling thread's ctx, or -1 (errno ENOMEM: all slots in use, or EIO:
-//  the ctx could not be created); release_session returns the slot.
+//  0) with thread_sessions slots (or ZMQG_THREAD_SESSIONS, up to 2^24: each
+//  slot is 64 bytes of device session table plus two 8-byte nonces).
+//  acquire_session returns 0 and a free slot of the calling thread's ctx, or
+//  -1 (errno ENOMEM: all slots in use, or EIO: the ctx could not be
+//  created); release_session returns the slot.  The drop-in
+//  zmq::curve_encoding_t turns a failure into a rejected connection, never an
+//  abort (zmq_curve_encoding.hpp).
 enum
 {
     thread_sessions = 4096

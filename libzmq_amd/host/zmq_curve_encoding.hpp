@@ -34,11 +34,17 @@ namespace zmq
 class curve_encoding_t
 {
   public:
+    //  The reference's constructor cannot fail.  Here a connection needs a
+    //  session slot of its I/O thread's device context; when none can be had
+    //  (all zmqg::thread_sessions slots in use: ENOMEM; no device context:
+    //  EIO) the object is still constructed, without a slot, and its encode
+    //  and decode fail (below), so the engine drops that one connection --
+    //  the process is never aborted for it.
     curve_encoding_t (const char *encode_nonce_prefix_,
                       const char *decode_nonce_prefix_,
                       const bool downgrade_sub_) :
-        _sid (acquire_sid ()),
-        _gpu (zmqg::thread_ctx (),
+        _sid_errno (acquire_sid (&_sid)),
+        _gpu (_sid_errno ? NULL : zmqg::thread_ctx (),
               _sid,
               encode_nonce_prefix_,
               decode_nonce_prefix_,
@@ -46,13 +52,23 @@ class curve_encoding_t
     {
     }
 
-    ~curve_encoding_t () { zmqg::release_session (_sid); }
+    ~curve_encoding_t ()
+    {
+        if (!_sid_errno)
+            zmqg::release_session (_sid);
+    }
 
     //  src/curve_mechanism_base.cpp:111-205: msg_ becomes the MESSAGE
     //  command (a fresh msg_t without flags, as msg_->move (msg_box) leaves
-    //  it).  -1 with errno set where the reference's rc would be non-zero.
+    //  it).  -1 with errno set where the reference's rc would be non-zero;
+    //  a connection without a session slot fails with EPROTO (the engine's
+    //  out_event stops pulling, src/stream_engine_base.cpp:331-339).
     int encode (msg_t *msg_)
     {
+        if (_sid_errno) {
+            errno = EPROTO;
+            return -1;
+        }
         zmqg::msg_buf_t m;
         const uint8_t *p = static_cast<const uint8_t *> (msg_->data ());
         m.bytes.assign (p, p + msg_->size ());
@@ -76,6 +92,14 @@ class curve_encoding_t
     //  them, with the peer nonce advanced as the reference advances it.
     int decode (msg_t *msg_, int *error_event_code_)
     {
+        if (_sid_errno) {
+            //  rejected like a frame that fails its MAC: the mechanism emits
+            //  the handshake-failed event and the engine closes this
+            //  connection (src/curve_mechanism_base.cpp:38-52)
+            *error_event_code_ = ZMQG_ERR_CRYPTOGRAPHIC; //  = ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC
+            errno = EPROTO;
+            return -1;
+        }
         zmqg::msg_buf_t m;
         const uint8_t *p = static_cast<const uint8_t *> (msg_->data ());
         m.bytes.assign (p, p + msg_->size ());
@@ -106,15 +130,15 @@ class curve_encoding_t
     }
 
   private:
-    static uint32_t acquire_sid ()
+    //  0 and *sid_ set, or the errno of zmqg::acquire_session
+    static int acquire_sid (uint32_t *sid_)
     {
-        uint32_t sid = 0;
-        const int rc = zmqg::acquire_session (&sid);
-        errno_assert (rc == 0);
-        return sid;
+        *sid_ = 0;
+        return zmqg::acquire_session (sid_) == 0 ? 0 : errno;
     }
 
-    const uint32_t _sid;
+    uint32_t _sid;
+    const int _sid_errno; //  0: this connection holds session slot _sid
     zmqg::curve_encoding_gpu_t _gpu;
 
     ZMQ_NON_COPYABLE_NOR_MOVABLE (curve_encoding_t)

@@ -1,8 +1,9 @@
 """GPU tests of the boundary's round-2 behaviour, against the CPU oracle:
 
-* in-place decode in the reference's two layouts (src/curve_mechanism_base.cpp:
-  222-260: plaintext where crypto_box_open_easy_afternm leaves it, and the
-  payload moved to the frame's start), for every frame-kernel variant and for
+* in-place decode in two layouts: each payload byte over its own ciphertext
+  byte (wire offset 33; the reference's open writes to message + 16 instead,
+  src/curve_mechanism_base.cpp:222-228), and the payload at the frame's start
+  as after the reference's memmove (:253-260), for every frame-kernel variant and for
   frames that take the chunked body path, with MAC and replay failures;
 * zmqg_*_batch_ex options: max_len (the body launches skipped, a broken bound
   reported as ZMQG_ERR_BOUND), encode status, session maxima;

@@ -1,0 +1,126 @@
+"""ZMQG_OPT_VERIFY_FIRST (include/zmqg_curve.h): decode writes `out` only
+after each frame's verdict, as libsodium's crypto_box_open_easy_afternm
+verifies before it decrypts (src/curve_mechanism_base.cpp:226-228).
+
+* Same results as the plain decode (statuses, flags, payloads, peer nonces)
+  on batches with MAC, header and replay failures, frames on both sides of
+  the frame kernel's 4.5 KiB range, separate and in-place layouts.
+* A second thread reading a pinned host `out` while forged batches are
+  decoded never sees a plaintext byte."""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import pack
+from tests.test_gpu_parity import dev, host
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(rng, sizes, precom, tamper_every=5):
+    n = len(sizes)
+    payloads = [rng.integers(0, 256, s, dtype=np.uint8).tobytes() for s in sizes]
+    inp, in_off = pack(payloads)
+    nonce = np.arange(3, 3 + n, dtype=np.uint64)
+    nonce[n // 2] = nonce[1]  # a replay
+    flags = (np.arange(n) % 3 == 0).astype(np.uint8)
+    wl = np.array([s + 33 for s in sizes], np.uint32)
+    wire_off = np.concatenate([[0], np.cumsum(wl)[:-1]]).astype(np.uint64)
+    sess = O.make_sessions([precom])
+    wire = O.encode_batch(sess, np.zeros(n, np.uint32), nonce, flags, in_off, np.array(sizes, np.uint32), inp,
+                          wire_off, int(wl.sum()))
+    for i in range(0, n, tamper_every):  # MAC failures
+        wire[wire_off[i] + 32 + (sizes[i] // 2)] ^= 0x40
+    wire[wire_off[n - 2] + 1] ^= 0x20  # broken command name
+    return wire, wire_off, wl, in_off
+
+
+@pytest.mark.parametrize("layout", ["separate", "inplace33", "inplace0"])
+def test_verify_first_matches_plain_decode(torch_cuda, C, layout):
+    torch = torch_cuda
+    rng = np.random.default_rng(90)
+    precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    sizes = [int(x) for x in rng.choice([0, 1, 31, 200, 1024, 4000, 4600, 9000, 70000], 240)]
+    wire, wire_off, wl, pay_off = _batch(rng, sizes, precom)
+    n = len(sizes)
+    results = []
+    for vf in (False, True):
+        dec = C.CurveContext(0, 1)
+        dec.session_set(0, precom, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+        d_wire = dev(torch, wire)
+        if layout == "separate":
+            out = torch.full((int(pay_off[-1]) + sizes[-1] + 64,), 0x77, dtype=torch.uint8, device="cuda")
+            out_off = pay_off
+        else:
+            out = d_wire
+            out_off = wire_off + (33 if layout == "inplace33" else 0)
+        fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(n, dtype=torch.int32, device="cuda")
+        dec.decode_batch(dev(torch, np.zeros(n, np.uint32)), dev(torch, wire_off), dev(torch, wl), d_wire,
+                         dev(torch, out_off), out, fl, st, verify_first=vf)
+        torch.cuda.synchronize()
+        results.append((host(out, np.uint8).copy(), host(fl, np.uint8), host(st, np.int32), dec.get_peer_nonce(0),
+                        out_off))
+    (o0, f0, s0, p0, off), (o1, f1, s1, p1, _) = results
+    assert (s0 != 0).sum() > n // 5
+    assert np.array_equal(s0, s1) and np.array_equal(f0, f1) and p0 == p1
+    for i in range(n):  # every payload region: the verified payload or zeros
+        a, b = int(off[i]), int(off[i]) + sizes[i]
+        if layout == "inplace0" and s0[i] != 0 and sizes[i] + 33 > 4608:
+            continue  # (plain decode zeroes that frame's whole wire region; verify-first its payload region)
+        assert np.array_equal(o0[a:b], o1[a:b]), (i, sizes[i], int(s0[i]))
+
+
+def test_reader_thread_never_sees_forged_plaintext(torch_cuda, C):
+    torch = torch_cuda
+    rng = np.random.default_rng(91)
+    precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    n, P = 16384, 1024
+    inp = np.full(n * P, 0xA5, np.uint8)  # a plaintext byte the reader can recognise
+    in_off = np.arange(n, dtype=np.uint64) * P
+    W = P + 33
+    wire_off = np.arange(n, dtype=np.uint64) * W
+    sess = O.make_sessions([precom])
+    wire = O.encode_batch(sess, np.zeros(n, np.uint32), np.arange(3, 3 + n, dtype=np.uint64), np.zeros(n, np.uint8),
+                          in_off, np.full(n, P, np.uint32), inp, wire_off, n * W)
+    wire[wire_off + 20] ^= 1  # every tag forged
+    dec = C.CurveContext(0, 1)
+    dec.session_set(0, precom, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    out = torch.zeros(n * P, dtype=torch.uint8).pin_memory()  # host memory the kernels write over PCIe
+    view = out.numpy()
+    d = [dev(torch, a) for a in (np.zeros(n, np.uint32), wire_off, np.full(n, W, np.uint32), wire, in_off)]
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+
+    def run(vf, reps=30):
+        seen = [0, 0]
+        stop = threading.Event()
+
+        def reader():
+            r = np.random.default_rng(5)
+            while not stop.is_set():
+                idx = r.integers(0, n * P, 4096)
+                seen[0] += int((view[idx] == 0xA5).sum())
+                seen[1] += 1
+
+        th = threading.Thread(target=reader)
+        th.start()
+        try:
+            for _ in range(reps):
+                dec.decode_batch(d[0], d[1], d[2], d[3], d[4], out, fl, st, verify_first=vf)
+                torch.cuda.synchronize()
+        finally:
+            stop.set()
+            th.join()
+        assert (host(st, np.int32) == 0x11000001).all()  # ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC
+        assert not (view == 0xA5).any()  # zero-filled at completion either way
+        return seen
+
+    exposed_plain = run(False)
+    exposed_vf = run(True)
+    print(f"plain decode: {exposed_plain[0]} plaintext bytes seen in {exposed_plain[1]} samples; "
+          f"verify-first: {exposed_vf[0]} in {exposed_vf[1]}")
+    assert exposed_vf[1] > 10
+    assert exposed_vf[0] == 0

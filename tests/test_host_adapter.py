@@ -95,3 +95,34 @@ def test_batcher_matches_per_message_path_and_oracle(tmp_path):
         assert ref.tobytes() == wire
         checked += 1
     assert checked == len(recs) > 1000
+
+
+def build_binding_test(out_dir):
+    """zmq_curve_encoding.hpp (the drop-in zmq::curve_encoding_t) over the
+    msg_t test double of tests/host/msg_model (see its header)."""
+    exe = os.path.join(out_dir, "test_zmq_binding")
+    cmd = ["g++", "-O2", "-std=c++11", "-Wall", "-Werror", "-o", exe,
+           "-I" + os.path.join(ROOT, "tests", "host", "msg_model"),
+           "-I" + os.path.join(ROOT, "libzmq_amd", "host"),
+           os.path.join(ROOT, "tests", "host", "test_zmq_binding.cpp"),
+           os.path.join(ROOT, "libzmq_amd", "host", "curve_encoding_gpu.cpp"),
+           "-L" + LIB_DIR, "-lzmqg_curve", "-Wl,-rpath," + LIB_DIR,
+           "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib"]
+    subprocess.check_call(cmd)
+    return exe
+
+
+def test_binding_compiles_and_links(tmp_path):
+    assert os.path.exists(build_binding_test(str(tmp_path)))
+
+
+@pytest.mark.gpu
+def test_binding_runs_on_msg_t(tmp_path):
+    """the four unittest_curve_encoding.cpp round trips on msg_t
+    objects (VSM / LMSG split, move, shrink, set_flags OR), subscribe, a
+    tampered box, and a connection without a session slot (no abort)."""
+    exe = build_binding_test(str(tmp_path))
+    env = dict(os.environ, ZMQG_THREAD_SESSIONS="4")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert r.stdout.strip() == "OK 14"
