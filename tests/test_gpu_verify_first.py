@@ -109,6 +109,7 @@ def test_reader_thread_never_sees_forged_plaintext(torch_cuda, C):
         th.start()
         try:
             for _ in range(reps):
+                dec.set_peer_nonce(0, 2)  # (each rep fails on its MACs, not as replays of the last)
                 dec.decode_batch(d[0], d[1], d[2], d[3], d[4], out, fl, st, verify_first=vf)
                 torch.cuda.synchronize()
         finally:
