@@ -1,0 +1,535 @@
+// curve_frames_st.hpp -- the one-lane-per-frame kernel with its global
+// traffic moved in coalesced 128-byte runs through LDS (k_frames_st).
+//
+// Same frame semantics as k_frames_seq / k_frames_lds (curve_frames.hpp,
+// curve_frames_lds.hpp): one lane owns one frame and walks its 64-byte
+// keystream windows in order with the sequential radix-2^32 Poly1305; the
+// decode header checks and replay rule of src/curve_mechanism_base.cpp:80-284
+// and src/mechanism_base.cpp:14-25; encode per :111-205.
+//
+// Why.  In k_frames_seq every lane loads and stores its own frame, so each
+// dwordx4 instruction touches 64 different 64-byte pieces; the address unit
+// takes ~700 (load) and ~970 (store) cycles per such instruction
+// (profiles/valu_rates_r02.md, vmem_issue), i.e. ~6.7 k cycles of memory
+// pipe per window against ~4.8 k of keystream and MAC -- memory alone ran as
+// long as the whole kernel (ablations).  With 8 or 16
+// lanes on one contiguous piece the same instruction costs a few cycles.
+// k_frames_lds moved 64-byte windows in 80-byte covers (5 and 4 lanes per
+// piece) and used unaligned ds_read/ds_write_b128, which gfx950 replays at
+// ~64 cycles each (cdna_hip_programming.md, Guideline 17); this kernel uses
+// only naturally aligned DS accesses beside the DMA.
+//
+// Super-steps.  Super-step K covers stream bytes [128K, 128K + 128), i.e.
+// windows 2K and 2K + 1 (window 0, with the header, nonce and tag, is read
+// by its lane directly).  Per wave:
+//   * input: the 16-byte-aligned cover of super-step K (9 granules = 144
+//     bytes per frame, 64 frames = 9 LDS-DMA instructions, consecutive
+//     lanes on consecutive granules of a frame: 9 lanes per piece) lands in
+//     input buffer K & 1; it is issued at the top of super-step K - 1, so a
+//     whole super-step (two keystream blocks) covers its latency.  The
+//     owning lane reads its window's 17 dwords with aligned ds_read_b32 and
+//     shifts them in registers (v_alignbyte).
+//   * output: the owning lane writes its window's 64 output bytes, shifted
+//     to the destination's 4-byte phase, as 17 aligned dwords into its
+//     frame's ring (256 bytes + 16 of overflow; output byte q of the frame,
+//     counted from the 16-byte boundary at or below its first byte, sits at
+//     ring byte q mod 256; an odd super-step's last bytes land in the
+//     overflow and are copied to [0, 16) at the top of the next even one).
+//     At the top of super-step K + 1 the wave reads the ring's 8 granules
+//     of super-step K (aligned ds_read_b128) and, after the next window's
+//     keystream, stores them as 8 dwordx4 instructions of 8 lanes per
+//     128-byte piece: whole granules only.  A frame's first and last
+//     partial granules (when its output does not start or end on a 16-byte
+//     boundary) go out by their own lane (granule_store_part); encode's
+//     header, nonce and tag at the end (store_bytes_c<32>).
+// LDS per wave: 2 x 9,216 (input) + 64 x 272 (rings) = 35,840 bytes; four
+// waves per workgroup, one workgroup per CU.
+#pragma once
+
+#include "curve_frames_lds.hpp"
+
+namespace zmqg {
+
+constexpr uint32_t kSxCover = 144;                         // a super-step's 16-byte-aligned input cover per frame
+constexpr uint32_t kSxInBuf = 64 * kSxCover;               // one input buffer per wave (9 DMA instructions)
+constexpr uint32_t kSxRing = 272;                          // output ring per frame: 256 + 16 overflow
+constexpr uint32_t kSxWave = 2 * kSxInBuf + 64 * kSxRing;  // 35,840 bytes
+static_assert(kFramesWaves * kSxWave <= 160u * 1024u, "LDS of one workgroup");
+
+
+template <bool DEC, class BigOp>
+__global__ __launch_bounds__(kFramesBS) void k_frames_st(
+    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
+    const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
+    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
+    uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
+    ReplayOut rp, BigOp big, ZState *__restrict__ zs, FrameCtl ctl)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t sx_lds[kFramesWaves * kSxWave];
+    const bool lb = DEC && rp.lb_flag != nullptr;
+    __shared__ unsigned long long sh_wmax[kFramesWaves];
+    __shared__ CallState sh_cs;
+    const bool use_ticket = lb && !rp.ordered; // (kernel-uniform)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+
+    // ---- the frame's descriptors, session key and first window (as in
+    // k_frames_seq: without a ticket these go out before the call state's
+    // round trip)
+    uint32_t i = 0, ii = 0, s = 0, L_in = 0;
+    bool valid = false, sid_ok = false, over = false;
+    const uint8_t *src = nullptr;
+    uint8_t *dst = nullptr;
+    uint32_t key[8];
+    uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
+    uint64_t A = 0, B = 0;
+    int32_t status = 0;
+    uint32_t hw[3] = {0, 0, 0};
+    uint32_t x0[16]; // window 0's stream words (decode: the wire; encode: payload bytes 0..31)
+    auto fetch = [&](uint32_t wgv) {
+        i = wgv * kFramesBS + threadIdx.x;
+        valid = i < n;
+        ii = valid ? i : n - 1;
+        sid_ok = sid[ii] < max_sessions;
+        s = sid_ok ? sid[ii] : 0u; // (a frame of an unknown session is not processed)
+        const DevSession &ses = sessions[s];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            key[t] = DEC ? ses.dec_key[t] : ses.enc_key[t];
+        src = in + in_off[ii];
+        dst = out + out_off[ii];
+        L_in = len[ii];
+        over = ctl.max_len != 0 && L_in > ctl.max_len; // the caller's bound broken
+        if (!DEC) {
+            hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
+            S = sid_ok && !over ? 32u + hl + L_in : 0u;
+            A = (uint64_t) (uintptr_t) src - 32u - hl;
+            B = (uint64_t) (uintptr_t) dst;
+            if (L_in >= 32u) { // payload bytes 0..31: two dwordx4 (and a dword when unaligned)
+                load_bytes_c<32>(src, x0);
+#pragma unroll
+                for (int k = 8; k < 16; ++k)
+                    x0[k] = 0;
+            } else {
+                load_window(src, (int) L_in, x0);
+            }
+        } else {
+            A = (uint64_t) (uintptr_t) src;
+            uint32_t d[17];
+            frame_load_raw(A, 0, L_in, d);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                x0[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], (uint32_t) A & 3u);
+            B = (uint64_t) (uintptr_t) dst - 33u;
+        }
+    };
+    CallState c0{};
+    if (threadIdx.x == 0) {
+        c0.epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c0.ticket = use_ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
+        c0.nbase = DEC ? 0ull : nonce_base(ctl);
+    }
+    if (!use_ticket)
+        fetch(blockIdx.x);
+    if (threadIdx.x == 0)
+        sh_cs = c0;
+    __syncthreads();
+    const CallState cs = sh_cs;
+    const uint32_t epoch = cs.epoch;
+    const uint32_t wg = use_ticket ? cs.ticket : blockIdx.x;
+    if (use_ticket)
+        fetch(wg);
+    const uint64_t nbase = cs.nbase;
+    unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
+
+    if (!DEC) {
+        const uint64_t nc = frame_nonce(nonce, ctl, nbase, ii);
+        n0 = bswap32((uint32_t) (nc >> 32));
+        n1 = bswap32((uint32_t) nc);
+    } else {
+        if (L_in < 64u)
+            mask_tail(x0, (int) L_in);
+        // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
+        const uint32_t b0 = x0[0] & 0xffu;
+        if (L_in <= 1u || L_in <= b0)
+            status = ZMQG_ERR_MALFORMED_UNSPECIFIED;
+        else if (L_in < 8u || x0[0] != 0x53454d07u || x0[1] != 0x45474153u)
+            status = ZMQG_ERR_UNEXPECTED_COMMAND;
+        else if (L_in < 33u)
+            status = ZMQG_ERR_MALFORMED_MESSAGE;
+        if (!sid_ok)
+            status = ZMQG_ERR_SESSION;
+        if (over)
+            status = ZMQG_ERR_BOUND;
+        n0 = x0[2];
+        n1 = x0[3];
+        S = status == 0 ? L_in : 0u;
+    }
+    const bool small = valid && S <= max_stream;
+    unsigned long long vn = 0, wexcl = 0, psn = 0, wagg = 0;
+    if (DEC) {
+        vn = valid && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
+        psn = rp.peer[s];
+        if (valid && !lb) { // (several sessions: the replay tables' input)
+            rp.vout[i] = vn;
+            rp.psnap[i] = psn;
+            if (rp.iota)
+                rp.iota[i] = i;
+        }
+        if (lb) {
+            unsigned long long sc = vn;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const unsigned long long o = __shfl_up(sc, d);
+                if ((int) lane >= d)
+                    sc = o > sc ? o : sc;
+            }
+            const unsigned long long up = __shfl_up(sc, 1);
+            if (lane == 63)
+                sh_wmax[wv] = sc;
+            __syncthreads();
+            for (uint32_t k = 0; k < kFramesWaves; ++k) {
+                if (k < wv)
+                    wexcl = sh_wmax[k] > wexcl ? sh_wmax[k] : wexcl;
+                wagg = sh_wmax[k] > wagg ? sh_wmax[k] : wagg;
+            }
+            if (lane > 0)
+                wexcl = up > wexcl ? up : wexcl;
+            if (threadIdx.x == 0)
+                lookback_publish(rp.lb_flag + wg, rp.lb_agg + wg, wagg, epoch, 1);
+        }
+    }
+    const bool is_big = valid && !small && S > 0;
+    if (!small)
+        S = 0;
+    const uint32_t nw = (S + 63u) >> 6;
+    uint32_t mx = nw;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = __shfl_xor(mx, d);
+        mx = o > mx ? o : mx;
+    }
+    const uint32_t steps = __builtin_amdgcn_readfirstlane(mx); // windows of the wave's longest frame
+    const uint32_t KS = (steps + 1u) >> 1;                       // super-steps
+
+    // ---- the wave's staging areas
+    uint8_t *const wlds = sx_lds + wv * kSxWave;
+    const uint32_t wlds_off =
+        __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (StLdsVoid *) wlds); // the wave's LDS byte offset
+    uint8_t *const ring = wlds + 2u * kSxInBuf;
+    uint8_t *const myring = ring + kSxRing * lane;
+    const uint32_t va = (uint32_t) A & 15u; // input phase: stream byte 0 at cover byte va
+    const uint32_t ub = (uint32_t) B & 15u; // output phase: output byte q = ub + stream byte
+    const uint32_t u4 = ub & 3u, up = u4 ? u4 : 4u;
+    const uint32_t lo = DEC ? 33u : 32u; // first stream byte of the cooperatively stored output
+    // output q ranges (q = ub + stream byte, from the 16-byte boundary Bg):
+    // head [hs, he) by this lane, whole granules [ga, gb) by the wave, tail
+    // [ts, te) by this lane
+    const uint32_t te = S > lo ? ub + S : 0u, hs = ub + lo;
+    const uint32_t hr = (hs + 15u) & ~15u;
+    const uint32_t he = te ? (hr < te ? hr : te) : 0u;
+    uint32_t ga = 0, gb = 0;
+    if (te && (te >> 4) > (hr >> 4)) {
+        ga = hr >> 4;
+        gb = te >> 4;
+    }
+    const uint32_t tsf = te & ~15u;
+    const uint32_t ts = te ? (tsf > he ? tsf : he) : 0u;
+
+    // DMA lanes: instruction j, lane -> granule k of frame f (idx = 64 j + lane = 9 f + k)
+    uint64_t dga[9];
+    int32_t dlim[9];
+    uint32_t dlow = 0; // bit j: granule k < 4 (window 0's part of super-step 0: read by its lane)
+    {
+        const uint64_t A16 = A - va;
+        const int32_t lim = S ? (int32_t) (S + va) : 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 9; ++j) {
+            const uint32_t idx = 64u * j + lane, f = idx / 9u, k = idx - 9u * f;
+            dga[j] = shfl_u64(A16, f) + 16u * k;
+            dlim[j] = __shfl(lim, (int) f) - (int32_t) (16u * k);
+            dlow |= (k < 4u ? 1u : 0u) << j;
+        }
+    }
+    auto dma = [&](uint32_t K) { // super-step K's cover -> input buffer K & 1 (no wait)
+        const uint32_t b = wlds_off + (K & 1u) * kSxInBuf;
+#pragma unroll
+        for (uint32_t j = 0; j < 9; ++j)
+            if ((int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u)))
+                lds_dma16(dga[j] + 128ull * K, b + 1024u * j);
+    };
+    // store lanes: instruction j, lane -> granule k = lane & 7 of frame f = 8 j + lane / 8
+    uint64_t sga[8];
+    uint32_t srg[8];
+    int32_t sglo[8], sghi[8];
+    {
+        const uint64_t Bg = B - ub;
+        const uint32_t k = lane & 7u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t f = 8u * j + (lane >> 3);
+            sga[j] = shfl_u64(Bg, f) + 16u * k;
+            srg[j] = kSxRing * f + 16u * k;
+            sglo[j] = __shfl((int) ga, (int) f) - (int32_t) k;
+            sghi[j] = __shfl((int) gb, (int) f) - (int32_t) k;
+        }
+    }
+    // super-step K's ring granules (half K & 1) -> registers; then to memory
+    auto coop_read = [&](uint32_t K, u32x4 (&sv)[8]) {
+        const uint32_t half = 128u * (K & 1u);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            sv[j] = *(const u32x4 *) (ring + srg[j] + half);
+    };
+    auto coop_store = [&](uint32_t K, const u32x4 (&sv)[8]) {
+        const int32_t g = (int32_t) (8u * K);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            if (g >= sglo[j] && g < sghi[j])
+                *(GU4 *) (uintptr_t) (sga[j] + 128ull * K) = sv[j];
+    };
+    // window w's output words y (ycarry: the previous window's last word) ->
+    // the ring, 17 aligned dwords at the destination's 4-byte phase (the
+    // first only when it merges the carry)
+    auto ring_put = [&](uint32_t K, uint32_t h, const uint32_t y[16], uint32_t ycarry) {
+        // r1: the dword holding output byte q0 + 4 - up (q0: the window's
+        // first), i.e. word 1 of the shifted window
+        uint32_t *const r1 = (uint32_t *) (myring + (128u * (K & 1u) + 64u * h + ub + 4u - up));
+        const uint32_t sft = 4u - up;
+        if (up != 4u)
+            r1[-1] = __builtin_amdgcn_alignbyte(y[0], ycarry, sft);
+#pragma unroll
+        for (int m = 1; m < 16; ++m)
+            r1[m - 1] = __builtin_amdgcn_alignbyte(y[m], y[m - 1], sft);
+        r1[15] = __builtin_amdgcn_alignbyte(0u, y[15], sft);
+    };
+
+    if (KS > 0u && steps > 1u)
+        dma(0u); // window 1's cover
+
+    // ---- window 0 (Poly1305 key, first 32 ciphertext bytes, header)
+    PolyKey32 pk;
+    Poly32 h = {0, 0, 0, 0, 0};
+    uint32_t spad[4], wtag[4] = {0, 0, 0, 0}, fl = 0;
+    uint32_t cp[16];                // ciphertext of the window whose MAC is absorbed next step
+    uint32_t cp_j0 = 2, cp_len = 0; // its first block slot and ciphertext bytes
+    uint32_t ycarry = 0;
+    {
+        uint32_t ks[16];
+        salsa20_block(ks, key, n0, n1, 0, 0);
+        pk = poly32_key(ks[0], ks[1], ks[2], ks[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            spad[k] = ks[4 + k];
+        uint32_t x[16];
+        if (DEC) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                x[k] = x0[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                wtag[k] = x[4 + k];
+        } else {
+            // plaintext bytes 0..31 = header || payload[0 .. 32-hl)
+            uint32_t pt[8];
+            switch (hl) {
+            case 1: shift_in<1>(x0, pt); break;
+            case 2: shift_in<2>(x0, pt); break;
+            case 8: shift_in<8>(x0, pt); break;
+            default: shift_in<11>(x0, pt); break;
+            }
+            pt[0] |= hw[0];
+            pt[1] |= hw[1];
+            pt[2] |= hw[2];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x[k] = 0;
+                x[8 + k] = pt[k];
+            }
+        }
+        uint32_t y[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            y[k] = x[k] ^ ks[k];
+        if (!DEC && S < 64u)
+            mask_tail(y, (int) S);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            cp[k] = DEC ? x[k] : y[k];
+        cp_len = (S < 64u ? S : 64u) - 32u; // (S = 0: unused)
+        if (DEC)
+            fl = y[8] & 3u;
+        if (nw > 0u)
+            ring_put(0u, 0u, y, 0u); // (the carry lands below the output: never stored)
+        ycarry = y[15];
+    }
+    call_state_count(zs);
+
+    // ---- windows 1 ..
+    auto window = [&](uint32_t K, uint32_t hh) {
+        const uint32_t t = 2u * K + hh;
+        const bool act = t < nw;
+        uint32_t d[17];
+        {
+            const uint32_t *const p =
+                (const uint32_t *) (wlds + (K & 1u) * kSxInBuf + kSxCover * lane + ((va + 64u * hh) & ~3u));
+#pragma unroll
+            for (int m = 0; m < 17; ++m)
+                d[m] = p[m];
+        }
+        uint32_t ks[16];
+        salsa20_block(ks, key, n0, n1, t, 0);
+        // The previous window's MAC, the four-block form for every lane in the
+        // keystream's basic block (see k_frames_seq); lanes whose window was
+        // not four full blocks keep h and take the general form below.
+        const bool pv = t - 1u < nw;
+        const bool full = pv && cp_j0 == 0u && cp_len == 64u;
+        {
+            Poly32 hf = h;
+            poly32_window_full(hf, pk, cp);
+            h.h0 = full ? hf.h0 : h.h0;
+            h.h1 = full ? hf.h1 : h.h1;
+            h.h2 = full ? hf.h2 : h.h2;
+            h.h3 = full ? hf.h3 : h.h3;
+            h.h4 = full ? hf.h4 : h.h4;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            asm volatile("" : "+v"(ks[k]));
+        asm volatile("" : "+v"(h.h0), "+v"(h.h1), "+v"(h.h2), "+v"(h.h3), "+v"(h.h4));
+        if (__builtin_amdgcn_ballot_w64(pv && !full) != 0) {
+            if (pv && !full)
+                poly32_window(h, pk, cp, cp_j0, cp_len);
+        }
+        uint32_t x[16];
+        const uint32_t sa = va & 3u;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            x[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sa);
+        const bool tail = act && S < 64u * t + 64u;
+        if (DEC && __builtin_amdgcn_ballot_w64(tail) != 0) {
+            if (tail)
+                mask_tail(x, (int) (S - 64u * t));
+        }
+        uint32_t y[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            y[k] = x[k] ^ ks[k];
+        if (!DEC && __builtin_amdgcn_ballot_w64(tail) != 0) {
+            if (tail)
+                mask_tail(y, (int) (S - 64u * t));
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            cp[k] = DEC ? x[k] : y[k];
+        cp_j0 = 0;
+        cp_len = act ? (S - 64u * t < 64u ? S - 64u * t : 64u) : 0u;
+        if (act)
+            ring_put(K, hh, y, ycarry);
+        ycarry = y[15];
+    };
+
+#pragma unroll 1
+    for (uint32_t K = 0; K < KS; ++K) {
+        // super-step K's cover has landed (issued a super-step ago), and the
+        // stores issued then are out of the way
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (K + 1u < KS)
+            dma(K + 1u);
+        u32x4 sv[8];
+        if (K > 0u)
+            coop_read(K - 1u, sv);
+        if ((K & 1u) == 0u && K > 0u && 2u * K < nw) { // the odd super-step's overflow -> [0, 16)
+            const u32x4 o = *(const u32x4 *) (myring + 256u);
+            *(u32x4 *) myring = o;
+        }
+        if (K > 0u)
+            window(K, 0u);
+        if (K > 0u)
+            coop_store(K - 1u, sv);
+        if (2u * K + 1u < steps)
+            window(K, 1u);
+        if (K == 0u && __builtin_amdgcn_ballot_w64(he > hs) != 0) {
+            // this lane's head: output bytes [hs, he) of granule hs / 16
+            if (he > hs) {
+                const uint32_t g = hs & ~15u;
+                const u32x4 v = *(const u32x4 *) (myring + g);
+                granule_store_part(B - ub + g, hs - g, he - g, v);
+            }
+        }
+    }
+    if (KS > 0u) {
+        // the last super-step's granules, then the lanes' tails
+        u32x4 sv[8];
+        coop_read(KS - 1u, sv);
+        coop_store(KS - 1u, sv);
+        if (__builtin_amdgcn_ballot_w64(te > ts) != 0) {
+            if (te > ts) {
+                const uint32_t Kf = (nw - 1u) >> 1; // this frame's last super-step
+                const uint32_t pos = 128u * (Kf & 1u) + (ts - 128u * Kf);
+                const u32x4 v = *(const u32x4 *) (myring + pos);
+                granule_store_part(B - ub + ts, 0u, te - ts, v);
+            }
+        }
+        // the last window's MAC
+        if (nw == steps)
+            poly32_window(h, pk, cp, cp_j0, cp_len);
+    }
+
+    unsigned long long excl = 0;
+    if (lb) {
+        const unsigned long long P = lookback_excl(wg, epoch, rp.lb_flag, rp.lb_agg, rp.lb_inc);
+        if (threadIdx.x == 0) {
+            const unsigned long long inc = P > wagg ? P : wagg;
+            if (gridDim.x > kFramesBS)
+                lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
+            if (wg + 1 == gridDim.x) {
+                *rp.peer = inc > psn ? inc : psn;
+                if (rp.smax)
+                    *rp.smax = inc;
+            }
+        }
+        excl = P > wexcl ? P : wexcl;
+        if (excl < psn)
+            excl = psn;
+    }
+    if (is_big && !ctl.no_body) {
+        if (lb) { // the body's finisher applies the rule to this frame
+            rp.excl[i] = excl;
+            rp.psnap[i] = psn;
+        }
+        big(i, list_ctr, nbase);
+    }
+    call_state_end<DEC>(zs, ctl, cs, n);
+    if (!DEC && valid && ctl.enc_status)
+        ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
+    if (!valid || !small)
+        return;
+    if (S == 0) { // decode: header failure (encode: a frame not processed)
+        if (DEC)
+            fail_unprocessed(status, L_in, dst, flags_out + i, status_out + i, zs, ctl);
+        return;
+    }
+    uint32_t tag[4];
+    poly32_finish(h, spad, tag);
+    if (!DEC) {
+        // "\x07MESSAGE" || nonce || tag: wire bytes 0..31 (the rest went out through the ring)
+        const uint32_t o[16] = {0x53454d07u, 0x45474153u, n0, n1, tag[0], tag[1], tag[2], tag[3]};
+        store_bytes_c<32>(dst, o);
+    } else {
+        if (lb && !(vn > excl))
+            status = ZMQG_ERR_INVALID_SEQUENCE; // src/curve_mechanism_base.cpp:99-104 (before the MAC)
+        else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
+            status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
+        status_out[i] = status;
+        flags_out[i] = status == 0 ? (uint8_t) fl : 0;
+        if (status != 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the wave's stores of this frame first
+            zero_bytes(dst, S - 33u);
+        }
+    }
+}
+
+} // namespace zmqg

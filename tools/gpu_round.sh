@@ -23,7 +23,7 @@ if [[ $MODE == all || $MODE == test ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
-  step bench 600 python bench.py --steps 50 --warmup 10
+  step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
 fi
 if [[ $MODE == all || $MODE == prof ]]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-staged --no-configs
