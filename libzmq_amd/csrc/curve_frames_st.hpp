@@ -1,5 +1,6 @@
 // curve_frames_st.hpp -- the one-lane-per-frame kernel with its global
-// traffic moved in coalesced 128-byte runs through LDS (k_frames_st).
+// traffic moved in coalesced 128-byte runs through LDS by a second wave on
+// each SIMD (k_frames_st).
 //
 // Same frame semantics as k_frames_seq / k_frames_lds (curve_frames.hpp,
 // curve_frames_lds.hpp): one lane owns one frame and walks its 64-byte
@@ -10,71 +11,90 @@
 // Why.  In k_frames_seq every lane loads and stores its own frame, so each
 // dwordx4 instruction touches 64 different 64-byte pieces; the address unit
 // takes ~700 (load) and ~970 (store) cycles per such instruction
-// (profiles/valu_rates_r02.md, vmem_issue), i.e. ~6.7 k cycles of memory
-// pipe per window against ~4.8 k of keystream and MAC -- memory alone ran as
-// long as the whole kernel (ablations).  With 8 or 16
-// lanes on one contiguous piece the same instruction costs a few cycles.
-// k_frames_lds moved 64-byte windows in 80-byte covers (5 and 4 lanes per
-// piece) and used unaligned ds_read/ds_write_b128, which gfx950 replays at
-// ~64 cycles each (cdna_hip_programming.md, Guideline 17); this kernel uses
-// only naturally aligned DS accesses beside the DMA.
+// (profiles/valu_rates_r02.md, vmem_issue): memory alone ran as long as the
+// whole kernel.  Moving the bytes in 128-byte runs
+// (8 or 9 lanes per piece) makes that cheap, but a single wave per SIMD that
+// also issues the moves and waits for them exposes every wait: a first
+// version of this kernel with one wave per SIMD doing both took 65 us at
+// config 2 against seq's 59 (memory and LDS work alone 42 us, compute alone
+// 51, ablations in DESIGN.md section 3.1).  So each SIMD holds two waves of
+// one 512-thread workgroup (waves w and w + 4 share a SIMD): a compute wave
+// (keystream, Poly1305, XOR; LDS reads and writes only) and its memory wave
+// (LDS-DMA loads, ring-to-global stores, the frames' edge bytes), meeting at
+// one workgroup barrier per super-step.  While one waits the other issues.
 //
 // Super-steps.  Super-step K covers stream bytes [128K, 128K + 128), i.e.
 // windows 2K and 2K + 1 (window 0, with the header, nonce and tag, is read
-// by its lane directly).  Per wave:
-//   * input: the 16-byte-aligned cover of super-step K (9 granules = 144
-//     bytes per frame, 64 frames = 9 LDS-DMA instructions, consecutive
-//     lanes on consecutive granules of a frame: 9 lanes per piece) lands in
-//     input buffer K & 1; it is issued at the top of super-step K - 1, so a
-//     whole super-step (two keystream blocks) covers its latency.  The
-//     owning lane reads its window's 17 dwords with aligned ds_read_b32 and
-//     shifts them in registers (v_alignbyte).
-//   * output: the owning lane writes its window's 64 output bytes, shifted
-//     to the destination's 4-byte phase, as 17 aligned dwords into its
-//     frame's ring (256 bytes + 16 of overflow; output byte q of the frame,
-//     counted from the 16-byte boundary at or below its first byte, sits at
-//     ring byte q mod 256; an odd super-step's last bytes land in the
-//     overflow and are copied to [0, 16) at the top of the next even one).
-//     At the top of super-step K + 1 the wave reads the ring's 8 granules
-//     of super-step K (aligned ds_read_b128) and, after the next window's
-//     keystream, stores them as 8 dwordx4 instructions of 8 lanes per
-//     128-byte piece: whole granules only.  A frame's first and last
-//     partial granules (when its output does not start or end on a 16-byte
-//     boundary) go out by their own lane (granule_store_part); encode's
-//     header, nonce and tag at the end (store_bytes_c<32>).
-// LDS per wave: 2 x 9,216 (input) + 64 x 272 (rings) = 35,840 bytes; four
-// waves per workgroup, one workgroup per CU.
+// by its lane directly).  Between barriers B_K and B_K+1:
+//   * compute wave: windows 2K, 2K+1 from input buffer K & 1 (the frame's
+//     16-byte-aligned cover of the super-step: 9 granules = 144 bytes at
+//     phase va; 17 aligned ds_read_b32 per window, shifted in registers);
+//     each window's 64 output bytes go, shifted to the destination's 4-byte
+//     phase, as aligned dwords into the frame's ring half K & 1; bytes past
+//     the half's end (the first bytes of super-step K+1's first granule) go
+//     to overflow slot K & 3.
+//   * memory wave: LDS-DMA of super-step K+1's covers into buffer (K+1) & 1
+//     (9 instructions, consecutive lanes on consecutive granules of a frame);
+//     super-step K-1's output granules from ring half (K-1) & 1 (granule 0
+//     completed from overflow slot (K-2) & 3) to memory as 8 dwordx4
+//     instructions of 8 lanes per 128-byte piece, whole granules only; after
+//     super-step 0 also each frame's partial first granule (head); then it
+//     waits for the DMA, so the compute wave finds the covers at B_K+1.
+// After the last super-step the memory wave stores the last granules and each
+// frame's partial last granule (tail), drains its stores and leaves; the
+// compute waves finish the MACs and the replay look-back (256 threads).
+// Only naturally aligned DS accesses (gfx950 replays misaligned b128 at ~64
+// cycles, cdna_hip_programming.md Guideline 17).
+// LDS per pair: 2 x 9,216 (input) + 64 x 336 (ring 256 + overflow 4 x 16 +
+// pad) = 39,936 bytes; four pairs per workgroup, one workgroup per CU.
 #pragma once
 
 #include "curve_frames_lds.hpp"
 
+#ifndef ZMQG_ST_ABLATE
+#define ZMQG_ST_ABLATE 0 // timing experiments only (outputs wrong): 1 no ring->global stores, 2 no DMA, 4 no ring
+                         // writes, 8 no window reads from LDS, 16 no Salsa20, 32 no Poly1305
+#endif
+
 namespace zmqg {
 
+constexpr uint32_t kSxThreads = 2 * kFramesBS;             // compute waves 0..3, memory waves 4..7
 constexpr uint32_t kSxCover = 144;                         // a super-step's 16-byte-aligned input cover per frame
-constexpr uint32_t kSxInBuf = 64 * kSxCover;               // one input buffer per wave (9 DMA instructions)
-constexpr uint32_t kSxRing = 272;                          // output ring per frame: 256 + 16 overflow
-constexpr uint32_t kSxWave = 2 * kSxInBuf + 64 * kSxRing;  // 35,840 bytes
-static_assert(kFramesWaves * kSxWave <= 160u * 1024u, "LDS of one workgroup");
+constexpr uint32_t kSxInBuf = 64 * kSxCover;               // one input buffer per pair (9 DMA instructions)
+constexpr uint32_t kSxRing = 336;                          // ring per frame: halves [0,256), overflow [256,320), pad
+constexpr uint32_t kSxPair = 2 * kSxInBuf + 64 * kSxRing;  // 39,936 bytes
+static_assert(kFramesWaves * kSxPair + 256 <= 160u * 1024u, "LDS of one workgroup");
 
+// byte mask of bytes [0, nb) of dword d of a granule (nb 0..16)
+__device__ __forceinline__ uint32_t lead_mask(uint32_t nb, uint32_t d)
+{
+    const int32_t b = (int32_t) nb - 4 * (int32_t) d;
+    return b >= 4 ? 0xffffffffu : b <= 0 ? 0u : (1u << (8 * b)) - 1u;
+}
 
 template <bool DEC, class BigOp>
-__global__ __launch_bounds__(kFramesBS) void k_frames_st(
+__global__ __launch_bounds__(kSxThreads) void k_frames_st(
     uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
     const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
     uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
     ReplayOut rp, BigOp big, ZState *__restrict__ zs, FrameCtl ctl)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t sx_lds[kFramesWaves * kSxWave];
-    const bool lb = DEC && rp.lb_flag != nullptr;
+    __shared__ __attribute__((aligned(16))) uint8_t sx_lds[kFramesWaves * kSxPair];
     __shared__ unsigned long long sh_wmax[kFramesWaves];
     __shared__ CallState sh_cs;
+    __shared__ uint32_t sh_steps[kFramesWaves];
+    const bool lb = DEC && rp.lb_flag != nullptr;
     const bool use_ticket = lb && !rp.ordered; // (kernel-uniform)
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const bool mem = wave >= kFramesWaves;          // (wave-uniform) the memory wave of pair wave & 3
+    const uint32_t wv = wave & (kFramesWaves - 1u); // the pair (= its compute wave)
+    uint8_t *const pl = sx_lds + wv * kSxPair;
+    const uint32_t pl_off = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (StLdsVoid *) pl);
+    uint8_t *const ring = pl + 2u * kSxInBuf;
+    uint8_t *const myring = ring + kSxRing * lane;
 
-    // ---- the frame's descriptors, session key and first window (as in
-    // k_frames_seq: without a ticket these go out before the call state's
-    // round trip)
+    // ---- compute waves: the frame's descriptors, session key, first window
     uint32_t i = 0, ii = 0, s = 0, L_in = 0;
     bool valid = false, sid_ok = false, over = false;
     const uint8_t *src = nullptr;
@@ -86,7 +106,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
     uint32_t hw[3] = {0, 0, 0};
     uint32_t x0[16]; // window 0's stream words (decode: the wire; encode: payload bytes 0..31)
     auto fetch = [&](uint32_t wgv) {
-        i = wgv * kFramesBS + threadIdx.x;
+        i = wgv * kFramesBS + wv * 64u + lane;
         valid = i < n;
         ii = valid ? i : n - 1;
         sid_ok = sid[ii] < max_sessions;
@@ -128,7 +148,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
         c0.ticket = use_ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
         c0.nbase = DEC ? 0ull : nonce_base(ctl);
     }
-    if (!use_ticket)
+    if (!mem && !use_ticket)
         fetch(blockIdx.x);
     if (threadIdx.x == 0)
         sh_cs = c0;
@@ -136,185 +156,289 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
     const CallState cs = sh_cs;
     const uint32_t epoch = cs.epoch;
     const uint32_t wg = use_ticket ? cs.ticket : blockIdx.x;
-    if (use_ticket)
+    if (!mem && use_ticket)
         fetch(wg);
     const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
 
-    if (!DEC) {
-        const uint64_t nc = frame_nonce(nonce, ctl, nbase, ii);
-        n0 = bswap32((uint32_t) (nc >> 32));
-        n1 = bswap32((uint32_t) nc);
-    } else {
-        if (L_in < 64u)
-            mask_tail(x0, (int) L_in);
-        // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
-        const uint32_t b0 = x0[0] & 0xffu;
-        if (L_in <= 1u || L_in <= b0)
-            status = ZMQG_ERR_MALFORMED_UNSPECIFIED;
-        else if (L_in < 8u || x0[0] != 0x53454d07u || x0[1] != 0x45474153u)
-            status = ZMQG_ERR_UNEXPECTED_COMMAND;
-        else if (L_in < 33u)
-            status = ZMQG_ERR_MALFORMED_MESSAGE;
-        if (!sid_ok)
-            status = ZMQG_ERR_SESSION;
-        if (over)
-            status = ZMQG_ERR_BOUND;
-        n0 = x0[2];
-        n1 = x0[3];
-        S = status == 0 ? L_in : 0u;
+    if (!mem) {
+        if (!DEC) {
+            const uint64_t nc = frame_nonce(nonce, ctl, nbase, ii);
+            n0 = bswap32((uint32_t) (nc >> 32));
+            n1 = bswap32((uint32_t) nc);
+        } else {
+            if (L_in < 64u)
+                mask_tail(x0, (int) L_in);
+            // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
+            const uint32_t b0 = x0[0] & 0xffu;
+            if (L_in <= 1u || L_in <= b0)
+                status = ZMQG_ERR_MALFORMED_UNSPECIFIED;
+            else if (L_in < 8u || x0[0] != 0x53454d07u || x0[1] != 0x45474153u)
+                status = ZMQG_ERR_UNEXPECTED_COMMAND;
+            else if (L_in < 33u)
+                status = ZMQG_ERR_MALFORMED_MESSAGE;
+            if (!sid_ok)
+                status = ZMQG_ERR_SESSION;
+            if (over)
+                status = ZMQG_ERR_BOUND;
+            n0 = x0[2];
+            n1 = x0[3];
+            S = status == 0 ? L_in : 0u;
+        }
     }
     const bool small = valid && S <= max_stream;
     unsigned long long vn = 0, wexcl = 0, psn = 0, wagg = 0;
     if (DEC) {
-        vn = valid && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
-        psn = rp.peer[s];
-        if (valid && !lb) { // (several sessions: the replay tables' input)
-            rp.vout[i] = vn;
-            rp.psnap[i] = psn;
-            if (rp.iota)
-                rp.iota[i] = i;
+        if (!mem) {
+            vn = valid && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
+            psn = rp.peer[s];
+            if (valid && !lb) { // (several sessions: the replay tables' input)
+                rp.vout[i] = vn;
+                rp.psnap[i] = psn;
+                if (rp.iota)
+                    rp.iota[i] = i;
+            }
         }
-        if (lb) {
+        if (lb) { // (the barrier is the whole workgroup's)
             unsigned long long sc = vn;
+            if (!mem) {
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const unsigned long long o = __shfl_up(sc, d);
-                if ((int) lane >= d)
-                    sc = o > sc ? o : sc;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const unsigned long long o = __shfl_up(sc, d);
+                    if ((int) lane >= d)
+                        sc = o > sc ? o : sc;
+                }
+                if (lane == 63)
+                    sh_wmax[wv] = sc;
             }
             const unsigned long long up = __shfl_up(sc, 1);
-            if (lane == 63)
-                sh_wmax[wv] = sc;
             __syncthreads();
-            for (uint32_t k = 0; k < kFramesWaves; ++k) {
-                if (k < wv)
-                    wexcl = sh_wmax[k] > wexcl ? sh_wmax[k] : wexcl;
-                wagg = sh_wmax[k] > wagg ? sh_wmax[k] : wagg;
+            if (!mem) {
+                for (uint32_t k = 0; k < kFramesWaves; ++k) {
+                    if (k < wv)
+                        wexcl = sh_wmax[k] > wexcl ? sh_wmax[k] : wexcl;
+                    wagg = sh_wmax[k] > wagg ? sh_wmax[k] : wagg;
+                }
+                if (lane > 0)
+                    wexcl = up > wexcl ? up : wexcl;
+                if (threadIdx.x == 0)
+                    lookback_publish(rp.lb_flag + wg, rp.lb_agg + wg, wagg, epoch, 1);
             }
-            if (lane > 0)
-                wexcl = up > wexcl ? up : wexcl;
-            if (threadIdx.x == 0)
-                lookback_publish(rp.lb_flag + wg, rp.lb_agg + wg, wagg, epoch, 1);
         }
     }
     const bool is_big = valid && !small && S > 0;
     if (!small)
         S = 0;
-    const uint32_t nw = (S + 63u) >> 6;
-    uint32_t mx = nw;
+    // compute waves hand the frame's stream addresses and length to their
+    // memory wave through the frame's overflow slots (first written in
+    // super-step 0's second window, after barrier B_0)
+    if (!mem) {
+        uint32_t nwc = (S + 63u) >> 6;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(mx, d);
-        mx = o > mx ? o : mx;
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = __shfl_xor(nwc, d);
+            nwc = o > nwc ? o : nwc;
+        }
+        if (lane == 0)
+            sh_steps[wv] = nwc;
+        unsigned long long *const ho = (unsigned long long *) (myring + 256u);
+        ho[0] = A;
+        ho[1] = B;
+        ho[2] = S;
     }
-    const uint32_t steps = __builtin_amdgcn_readfirstlane(mx); // windows of the wave's longest frame
-    const uint32_t KS = (steps + 1u) >> 1;                       // super-steps
-
-    // ---- the wave's staging areas
-    uint8_t *const wlds = sx_lds + wv * kSxWave;
-    const uint32_t wlds_off =
-        __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (StLdsVoid *) wlds); // the wave's LDS byte offset
-    uint8_t *const ring = wlds + 2u * kSxInBuf;
-    uint8_t *const myring = ring + kSxRing * lane;
+    __syncthreads();
+    if (mem) {
+        const unsigned long long *const ho = (const unsigned long long *) (myring + 256u);
+        A = ho[0];
+        B = ho[1];
+        S = (uint32_t) ho[2];
+    }
+    uint32_t stw = 0; // this pair's windows (its longest frame)
+    uint32_t KS = 0;  // super-steps of the workgroup (every wave meets every barrier)
+#pragma unroll
+    for (uint32_t k = 0; k < kFramesWaves; ++k) {
+        const uint32_t v = sh_steps[k];
+        stw = k == wv ? v : stw;
+        KS = v > KS ? v : KS;
+    }
+    stw = __builtin_amdgcn_readfirstlane(stw);
+    KS = __builtin_amdgcn_readfirstlane((KS + 1u) >> 1);
+    const uint32_t nw = (S + 63u) >> 6;
     const uint32_t va = (uint32_t) A & 15u; // input phase: stream byte 0 at cover byte va
     const uint32_t ub = (uint32_t) B & 15u; // output phase: output byte q = ub + stream byte
     const uint32_t u4 = ub & 3u, up = u4 ? u4 : 4u;
-    const uint32_t lo = DEC ? 33u : 32u; // first stream byte of the cooperatively stored output
-    // output q ranges (q = ub + stream byte, from the 16-byte boundary Bg):
-    // head [hs, he) by this lane, whole granules [ga, gb) by the wave, tail
-    // [ts, te) by this lane
-    const uint32_t te = S > lo ? ub + S : 0u, hs = ub + lo;
-    const uint32_t hr = (hs + 15u) & ~15u;
-    const uint32_t he = te ? (hr < te ? hr : te) : 0u;
-    uint32_t ga = 0, gb = 0;
-    if (te && (te >> 4) > (hr >> 4)) {
-        ga = hr >> 4;
-        gb = te >> 4;
-    }
-    const uint32_t tsf = te & ~15u;
-    const uint32_t ts = te ? (tsf > he ? tsf : he) : 0u;
 
-    // DMA lanes: instruction j, lane -> granule k of frame f (idx = 64 j + lane = 9 f + k)
-    uint64_t dga[9];
-    int32_t dlim[9];
-    uint32_t dlow = 0; // bit j: granule k < 4 (window 0's part of super-step 0: read by its lane)
-    {
-        const uint64_t A16 = A - va;
-        const int32_t lim = S ? (int32_t) (S + va) : 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 9; ++j) {
-            const uint32_t idx = 64u * j + lane, f = idx / 9u, k = idx - 9u * f;
-            dga[j] = shfl_u64(A16, f) + 16u * k;
-            dlim[j] = __shfl(lim, (int) f) - (int32_t) (16u * k);
-            dlow |= (k < 4u ? 1u : 0u) << j;
-        }
-    }
-    auto dma = [&](uint32_t K) { // super-step K's cover -> input buffer K & 1 (no wait)
-        const uint32_t b = wlds_off + (K & 1u) * kSxInBuf;
-#pragma unroll
-        for (uint32_t j = 0; j < 9; ++j)
-            if ((int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u)))
-                lds_dma16(dga[j] + 128ull * K, b + 1024u * j);
-    };
-    // store lanes: instruction j, lane -> granule k = lane & 7 of frame f = 8 j + lane / 8
-    uint64_t sga[8];
-    uint32_t srg[8];
-    int32_t sglo[8], sghi[8];
-    {
-        const uint64_t Bg = B - ub;
-        const uint32_t k = lane & 7u;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) {
-            const uint32_t f = 8u * j + (lane >> 3);
-            sga[j] = shfl_u64(Bg, f) + 16u * k;
-            srg[j] = kSxRing * f + 16u * k;
-            sglo[j] = __shfl((int) ga, (int) f) - (int32_t) k;
-            sghi[j] = __shfl((int) gb, (int) f) - (int32_t) k;
-        }
-    }
-    // super-step K's ring granules (half K & 1) -> registers; then to memory
-    auto coop_read = [&](uint32_t K, u32x4 (&sv)[8]) {
-        const uint32_t half = 128u * (K & 1u);
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            sv[j] = *(const u32x4 *) (ring + srg[j] + half);
-    };
-    auto coop_store = [&](uint32_t K, const u32x4 (&sv)[8]) {
-        const int32_t g = (int32_t) (8u * K);
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            if (g >= sglo[j] && g < sghi[j])
-                *(GU4 *) (uintptr_t) (sga[j] + 128ull * K) = sv[j];
-    };
-    // window w's output words y (ycarry: the previous window's last word) ->
-    // the ring, 17 aligned dwords at the destination's 4-byte phase (the
-    // first only when it merges the carry)
-    auto ring_put = [&](uint32_t K, uint32_t h, const uint32_t y[16], uint32_t ycarry) {
-        // r1: the dword holding output byte q0 + 4 - up (q0: the window's
-        // first), i.e. word 1 of the shifted window
-        uint32_t *const r1 = (uint32_t *) (myring + (128u * (K & 1u) + 64u * h + ub + 4u - up));
-        const uint32_t sft = 4u - up;
-        if (up != 4u)
-            r1[-1] = __builtin_amdgcn_alignbyte(y[0], ycarry, sft);
-#pragma unroll
-        for (int m = 1; m < 16; ++m)
-            r1[m - 1] = __builtin_amdgcn_alignbyte(y[m], y[m - 1], sft);
-        r1[15] = __builtin_amdgcn_alignbyte(0u, y[15], sft);
-    };
-
-    if (KS > 0u && steps > 1u)
-        dma(0u); // window 1's cover
-
-    // ---- window 0 (Poly1305 key, first 32 ciphertext bytes, header)
     PolyKey32 pk;
     Poly32 h = {0, 0, 0, 0, 0};
     uint32_t spad[4], wtag[4] = {0, 0, 0, 0}, fl = 0;
+
+    if (mem) {
+        // ================================================================ memory wave
+        const uint32_t lo = DEC ? 33u : 32u; // first stream byte of the ring-stored output
+        // output q ranges (q = ub + stream byte, from the 16-byte boundary
+        // Bg): head [hs, he) and tail [ts, te) by this lane, whole granules
+        // [ga, gb) by the wave
+        const uint32_t te = S > lo ? ub + S : 0u, hs = ub + lo;
+        const uint32_t hr = (hs + 15u) & ~15u;
+        const uint32_t he = te ? (hr < te ? hr : te) : 0u;
+        uint32_t ga = 0, gb = 0;
+        if (te && (te >> 4) > (hr >> 4)) {
+            ga = hr >> 4;
+            gb = te >> 4;
+        }
+        const uint32_t tsf = te & ~15u;
+        const uint32_t ts = te ? (tsf > he ? tsf : he) : 0u;
+        const uint64_t Bg = B - ub;
+
+        // DMA lanes: instruction j, lane -> granule k of frame f (idx = 64 j + lane = 9 f + k)
+        uint64_t dga[9];
+        int32_t dlim[9];
+        uint32_t dlow = 0; // bit j: granule k < 4 (window 0's part of super-step 0: read by its lane)
+        {
+            const uint64_t A16 = A - va;
+            const int32_t lim = S ? (int32_t) (S + va) : 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 9; ++j) {
+                const uint32_t idx = 64u * j + lane, f = idx / 9u, k = idx - 9u * f;
+                dga[j] = shfl_u64(A16, f) + 16u * k;
+                dlim[j] = __shfl(lim, (int) f) - (int32_t) (16u * k);
+                dlow |= (k < 4u ? 1u : 0u) << j;
+            }
+        }
+        auto dma = [&](uint32_t K) { // super-step K's covers -> input buffer K & 1 (no wait)
+            const uint32_t b = pl_off + (K & 1u) * kSxInBuf;
+#pragma unroll
+            for (uint32_t j = 0; j < 9; ++j)
+                if (!(ZMQG_ST_ABLATE & 2) && (int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u)))
+                    lds_dma16(dga[j] + 128ull * K, b + 1024u * j);
+        };
+        // store lanes: instruction j, lane -> granule k = lane & 7 of frame f = 8 j + lane / 8
+        const uint32_t sk = lane & 7u;
+        uint64_t sga[8];
+        uint32_t srg[8];
+        int32_t sglo[8], sghi[8];
+        uint32_t smask[8][4]; // k = 0 lanes: the bytes of granule 0 that come from the overflow slot
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t f = 8u * j + (lane >> 3);
+            sga[j] = shfl_u64(Bg, f) + 16u * sk;
+            srg[j] = kSxRing * f + 16u * sk;
+            sglo[j] = __shfl((int) ga, (int) f) - (int32_t) sk;
+            sghi[j] = __shfl((int) gb, (int) f) - (int32_t) sk;
+            const uint32_t ubf = (uint32_t) __shfl((int) ub, (int) f);
+#pragma unroll
+            for (uint32_t d = 0; d < 4; ++d)
+                smask[j][d] = lead_mask(ubf, d);
+        }
+        // super-step K's ring granules -> memory (granule 0 completed from
+        // super-step K-1's overflow slot)
+        auto coop = [&](uint32_t K) {
+            const uint32_t half = 128u * (K & 1u), ovf = 256u + 16u * ((K - 1u) & 3u);
+            u32x4 sv[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j)
+                sv[j] = *(const u32x4 *) (ring + srg[j] + half);
+            if (K > 0u && sk == 0u) {
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) {
+                    const u32x4 o = *(const u32x4 *) (ring + srg[j] + ovf);
+                    sv[j].x = (o.x & smask[j][0]) | (sv[j].x & ~smask[j][0]);
+                    sv[j].y = (o.y & smask[j][1]) | (sv[j].y & ~smask[j][1]);
+                    sv[j].z = (o.z & smask[j][2]) | (sv[j].z & ~smask[j][2]);
+                    sv[j].w = (o.w & smask[j][3]) | (sv[j].w & ~smask[j][3]);
+                }
+            }
+            const int32_t g = (int32_t) (8u * K);
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j)
+                if (!(ZMQG_ST_ABLATE & 1) && g >= sglo[j] && g < sghi[j])
+                    *(GU4 *) (uintptr_t) (sga[j] + 128ull * K) = sv[j];
+        };
+        auto head = [&]() { // output bytes [hs, he) of granule hs / 16 (super-step 0, k >= 2)
+            if (__builtin_amdgcn_ballot_w64(he > hs) != 0) {
+                if (he > hs) {
+                    const uint32_t g = hs & ~15u;
+                    const u32x4 v = *(const u32x4 *) (myring + g);
+                    granule_store_part(Bg + g, hs - g, he - g, v);
+                }
+            }
+        };
+
+        if (KS > 0u)
+            dma(0u); // window 1's covers
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll 1
+        for (uint32_t K = 0; K < KS; ++K) {
+            __syncthreads(); // B_K: super-step K's covers are in; super-step K-1's ring is complete
+            if (K + 1u < KS)
+                dma(K + 1u);
+            if (K > 0u)
+                coop(K - 1u);
+            if (K == 1u)
+                head();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the DMA, before B_K+1
+        }
+        __syncthreads(); // B_KS: the last super-step's ring is complete
+        if (KS > 0u) {
+            coop(KS - 1u);
+            if (KS == 1u)
+                head();
+            if (__builtin_amdgcn_ballot_w64(te > ts) != 0) {
+                if (te > ts) { // output bytes [ts, te) of granule ts / 16
+                    const uint32_t G = ts >> 4, Kg = G >> 3, k = G & 7u;
+                    u32x4 v = *(const u32x4 *) (myring + 128u * (Kg & 1u) + 16u * k);
+                    if (k == 0u) {
+                        const u32x4 o = *(const u32x4 *) (myring + 256u + 16u * ((Kg - 1u) & 3u));
+                        const uint32_t m0 = lead_mask(ub, 0), m1 = lead_mask(ub, 1), m2 = lead_mask(ub, 2),
+                                       m3 = lead_mask(ub, 3);
+                        v.x = (o.x & m0) | (v.x & ~m0);
+                        v.y = (o.y & m1) | (v.y & ~m1);
+                        v.z = (o.z & m2) | (v.z & ~m2);
+                        v.w = (o.w & m3) | (v.w & ~m3);
+                    }
+                    granule_store_part(Bg + ts, 0u, te - ts, v);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every store of the frames drained before B_fin
+        __syncthreads();                                 // B_fin
+        return;
+    }
+
+    // ==================================================================== compute wave
+    // window w's output words y (ycarry: the previous window's last word) ->
+    // ring half K & 1 as aligned dwords at the destination's 4-byte phase
+    // (the first only when it merges the carry); a second window's dwords
+    // past the half's end -> overflow slot K & 3
+    auto ring_put = [&](uint32_t K, uint32_t hh, const uint32_t y[16], uint32_t ycarry) {
+        if (ZMQG_ST_ABLATE & 4)
+            return;
+        const uint32_t P0 = 128u * (K & 1u) + 64u * hh + ub - up; // dword 0's position
+        const uint32_t hend = 128u * (K & 1u) + 128u, ovf = 256u + 16u * (K & 3u);
+        const uint32_t sft = 4u - up;
+        uint32_t o[17];
+        o[0] = __builtin_amdgcn_alignbyte(y[0], ycarry, sft);
+#pragma unroll
+        for (int m = 1; m < 16; ++m)
+            o[m] = __builtin_amdgcn_alignbyte(y[m], y[m - 1], sft);
+        o[16] = __builtin_amdgcn_alignbyte(0u, y[15], sft);
+        if (up != 4u)
+            *(uint32_t *) (myring + P0) = o[0];
+#pragma unroll
+        for (uint32_t m = 1; m < 17; ++m) {
+            uint32_t p = P0 + 4u * m;
+            if (hh == 1u && m >= 13u) // (dwords 0..12 of a second window never pass the half's end)
+                p = p >= hend ? p - hend + ovf : p;
+            *(uint32_t *) (myring + p) = o[m];
+        }
+    };
+
     uint32_t cp[16];                // ciphertext of the window whose MAC is absorbed next step
     uint32_t cp_j0 = 2, cp_len = 0; // its first block slot and ciphertext bytes
     uint32_t ycarry = 0;
+    // ---- window 0 (Poly1305 key, first 32 ciphertext bytes, header)
     {
         uint32_t ks[16];
         salsa20_block(ks, key, n0, n1, 0, 0);
@@ -373,13 +497,19 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
         uint32_t d[17];
         {
             const uint32_t *const p =
-                (const uint32_t *) (wlds + (K & 1u) * kSxInBuf + kSxCover * lane + ((va + 64u * hh) & ~3u));
+                (const uint32_t *) (pl + (K & 1u) * kSxInBuf + kSxCover * lane + ((va + 64u * hh) & ~3u));
 #pragma unroll
             for (int m = 0; m < 17; ++m)
-                d[m] = p[m];
+                d[m] = (ZMQG_ST_ABLATE & 8) ? key[m & 7] + t * 0x9e3779b9u + (uint32_t) m : p[m];
         }
         uint32_t ks[16];
-        salsa20_block(ks, key, n0, n1, t, 0);
+        if (ZMQG_ST_ABLATE & 16) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                ks[k] = key[k & 7] ^ (t * 0x9e3779b9u + k);
+        } else {
+            salsa20_block(ks, key, n0, n1, t, 0);
+        }
         // The previous window's MAC, the four-block form for every lane in the
         // keystream's basic block (see k_frames_seq); lanes whose window was
         // not four full blocks keep h and take the general form below.
@@ -387,7 +517,10 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
         const bool full = pv && cp_j0 == 0u && cp_len == 64u;
         {
             Poly32 hf = h;
-            poly32_window_full(hf, pk, cp);
+            if (ZMQG_ST_ABLATE & 32)
+                hf.h0 ^= cp[0] ^ cp[5] ^ cp[11];
+            else
+                poly32_window_full(hf, pk, cp);
             h.h0 = full ? hf.h0 : h.h0;
             h.h1 = full ? hf.h1 : h.h1;
             h.h2 = full ? hf.h2 : h.h2;
@@ -398,7 +531,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
         for (int k = 0; k < 16; ++k)
             asm volatile("" : "+v"(ks[k]));
         asm volatile("" : "+v"(h.h0), "+v"(h.h1), "+v"(h.h2), "+v"(h.h3), "+v"(h.h4));
-        if (__builtin_amdgcn_ballot_w64(pv && !full) != 0) {
+        if (!(ZMQG_ST_ABLATE & 32) && __builtin_amdgcn_ballot_w64(pv && !full) != 0) {
             if (pv && !full)
                 poly32_window(h, pk, cp, cp_j0, cp_len);
         }
@@ -432,57 +565,25 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
 
 #pragma unroll 1
     for (uint32_t K = 0; K < KS; ++K) {
-        // super-step K's cover has landed (issued a super-step ago), and the
-        // stores issued then are out of the way
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (K + 1u < KS)
-            dma(K + 1u);
-        u32x4 sv[8];
-        if (K > 0u)
-            coop_read(K - 1u, sv);
-        if ((K & 1u) == 0u && K > 0u && 2u * K < nw) { // the odd super-step's overflow -> [0, 16)
-            const u32x4 o = *(const u32x4 *) (myring + 256u);
-            *(u32x4 *) myring = o;
-        }
-        if (K > 0u)
+        __syncthreads(); // B_K: super-step K's covers have landed; the ring half is free
+        if (K > 0u && 2u * K < stw)
             window(K, 0u);
-        if (K > 0u)
-            coop_store(K - 1u, sv);
-        if (2u * K + 1u < steps)
+        if (2u * K + 1u < stw)
             window(K, 1u);
-        if (K == 0u && __builtin_amdgcn_ballot_w64(he > hs) != 0) {
-            // this lane's head: output bytes [hs, he) of granule hs / 16
-            if (he > hs) {
-                const uint32_t g = hs & ~15u;
-                const u32x4 v = *(const u32x4 *) (myring + g);
-                granule_store_part(B - ub + g, hs - g, he - g, v);
-            }
-        }
     }
-    if (KS > 0u) {
-        // the last super-step's granules, then the lanes' tails
-        u32x4 sv[8];
-        coop_read(KS - 1u, sv);
-        coop_store(KS - 1u, sv);
-        if (__builtin_amdgcn_ballot_w64(te > ts) != 0) {
-            if (te > ts) {
-                const uint32_t Kf = (nw - 1u) >> 1; // this frame's last super-step
-                const uint32_t pos = 128u * (Kf & 1u) + (ts - 128u * Kf);
-                const u32x4 v = *(const u32x4 *) (myring + pos);
-                granule_store_part(B - ub + ts, 0u, te - ts, v);
-            }
-        }
-        // the last window's MAC
-        if (nw == steps)
-            poly32_window(h, pk, cp, cp_j0, cp_len);
-    }
+    __syncthreads(); // B_KS
+    // the last window's MAC
+    if (stw > 0u && nw == stw)
+        poly32_window(h, pk, cp, cp_j0, cp_len);
+    __syncthreads(); // B_fin: the memory waves' stores of these frames are done; they have left
 
     unsigned long long excl = 0;
     if (lb) {
         const unsigned long long P = lookback_excl(wg, epoch, rp.lb_flag, rp.lb_agg, rp.lb_inc);
         if (threadIdx.x == 0) {
             const unsigned long long inc = P > wagg ? P : wagg;
+            // (a grid of at most kFramesBS workgroups looks back over every
+            // aggregate in one round and needs no inclusive values)
             if (gridDim.x > kFramesBS)
                 lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
             if (wg + 1 == gridDim.x) {
@@ -525,10 +626,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_st(
             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
         status_out[i] = status;
         flags_out[i] = status == 0 ? (uint8_t) fl : 0;
-        if (status != 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the wave's stores of this frame first
+        if (status != 0) // (the memory wave drained its stores of this frame before B_fin)
             zero_bytes(dst, S - 33u);
-        }
     }
 }
 

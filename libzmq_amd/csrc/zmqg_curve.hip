@@ -1805,7 +1805,7 @@ int frames_capacity(zmqg_ctx *ctx, int G)
     int &c = ctx->frames_cap[G == 16 ? 5 : G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0 : G == 2 ? 1 : 2];
     if (c == 0) {
         int nb = 0;
-        hipError_t e = G == 16  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_st<true, DecodeHead>, kFramesBS, 0)
+        hipError_t e = G == 16  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_st<true, DecodeHead>, kSxThreads, 0)
                        : G == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_lds<true, DecodeHead>, kFramesBS, 0)
                        : G == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
                        : G == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
@@ -1824,7 +1824,7 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
 {
     const dim3 grid((uint32_t) (((uint64_t) n * (G == 1 || G == 2 || G == 4 ? G : 1) + kFramesBS - 1) / kFramesBS));
     if (G == 16) {
-        hipLaunchKernelGGL((k_frames_st<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
+        hipLaunchKernelGGL((k_frames_st<DEC, BigOp>), grid, dim3(kSxThreads), 0, st, n, sid, nonce, flags, in_off, len, in,
                            out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
                            ctl);
         return;
