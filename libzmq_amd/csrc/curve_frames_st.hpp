@@ -56,6 +56,31 @@
                          // writes, 8 no window reads from LDS, 16 no Salsa20, 32 no Poly1305
 #endif
 
+#ifndef ZMQG_ST_MEMPRIO
+#define ZMQG_ST_MEMPRIO 2 // s_setprio of the memory waves (0: same as the compute waves)
+#endif
+
+#ifndef ZMQG_ST_STAMPS
+#define ZMQG_ST_STAMPS 0 // diagnostic builds only (tools/st_stamps.hip): per-wave s_memtime stamps into rp.clk
+#endif
+#if ZMQG_ST_STAMPS
+#define ST_STAMP(slot)                                                                                        \
+    do {                                                                                                      \
+        if (rp.clk && (threadIdx.x & 63u) == 0 && (slot) < 64u)                                               \
+            rp.clk[64ull * (blockIdx.x * (kSxThreads / 64) + (threadIdx.x >> 6)) + (slot)] =                  \
+                __builtin_amdgcn_s_memtime();                                                                 \
+    } while (0)
+#define ST_RTSTAMP(slot)                                                                                      \
+    do {                                                                                                      \
+        if (rp.clk && (threadIdx.x & 63u) == 0)                                                               \
+            rp.clk[64ull * (blockIdx.x * (kSxThreads / 64) + (threadIdx.x >> 6)) + (slot)] =                  \
+                __builtin_amdgcn_s_memrealtime();                                                             \
+    } while (0)
+#else
+#define ST_STAMP(slot) do { } while (0)
+#define ST_RTSTAMP(slot) do { } while (0)
+#endif
+
 namespace zmqg {
 
 constexpr uint32_t kSxThreads = 2 * kFramesBS;             // compute waves 0..3, memory waves 4..7
@@ -93,6 +118,10 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
     const uint32_t pl_off = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (StLdsVoid *) pl);
     uint8_t *const ring = pl + 2u * kSxInBuf;
     uint8_t *const myring = ring + kSxRing * lane;
+    ST_STAMP(0u);
+    ST_RTSTAMP(62u);
+    if (mem && ZMQG_ST_MEMPRIO) // the memory wave's few VALU instructions go ahead of its partner's
+        __builtin_amdgcn_s_setprio(ZMQG_ST_MEMPRIO);
 
     // ---- compute waves: the frame's descriptors, session key, first window
     uint32_t i = 0, ii = 0, s = 0, L_in = 0;
@@ -142,22 +171,106 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
             B = (uint64_t) (uintptr_t) dst - 33u;
         }
     };
+    // memory waves: the same frame's descriptors without the key and window
+    // 0; decode's S is provisional (before the header checks, which only
+    // ever zero it) -- enough to load the covers, and the same on both roles
+    auto fetch_mem = [&](uint32_t wgv) {
+        i = wgv * kFramesBS + wv * 64u + lane;
+        valid = i < n;
+        ii = valid ? i : n - 1;
+        sid_ok = sid[ii] < max_sessions;
+        s = sid_ok ? sid[ii] : 0u;
+        const uint8_t *const sp = in + in_off[ii];
+        uint8_t *const dp = out + out_off[ii];
+        L_in = len[ii];
+        over = ctl.max_len != 0 && L_in > ctl.max_len;
+        if (!DEC) {
+            hl = plaintext_header(flags[ii], sessions[s].downgrade_sub, hw);
+            S = sid_ok && !over ? 32u + hl + L_in : 0u;
+            A = (uint64_t) (uintptr_t) sp - 32u - hl;
+            B = (uint64_t) (uintptr_t) dp;
+        } else {
+            S = sid_ok && !over ? L_in : 0u;
+            A = (uint64_t) (uintptr_t) sp;
+            B = (uint64_t) (uintptr_t) dp - 33u;
+        }
+    };
+    // every wave's provisional window count -> sh_steps (the workgroup's
+    // super-step count: every wave meets every barrier)
+    auto publish_steps = [&]() {
+        const uint32_t Sp = (DEC && !mem) ? (sid_ok && !over ? L_in : 0u) : S;
+        uint32_t w = valid && Sp <= max_stream ? (Sp + 63u) >> 6 : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = __shfl_xor(w, d);
+            w = o > w ? o : w;
+        }
+        if (lane == 0)
+            sh_steps[wave] = w;
+    };
+    // memory waves: DMA lanes -- instruction j, lane -> granule k of frame f
+    // (idx = 64 j + lane = 9 f + k); the first covers go out at once
+    uint64_t dga[9];
+    int32_t dlim[9];
+    uint32_t dlow = 0; // bit j: granule k < 4 (window 0's part of super-step 0: read by its lane)
+    auto dma = [&](uint32_t K) { // super-step K's covers -> input buffer K & 1 (no wait)
+        const uint32_t b = pl_off + (K & 1u) * kSxInBuf;
+#pragma unroll
+        for (uint32_t j = 0; j < 9; ++j)
+            if (!(ZMQG_ST_ABLATE & 2) && (int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u)))
+                lds_dma16(dga[j] + 128ull * K, b + 1024u * j);
+    };
+    auto mem_start = [&]() {
+        const uint32_t vv = (uint32_t) A & 15u;
+        const uint64_t A16 = A - vv;
+        const int32_t lim = valid && S <= max_stream && S ? (int32_t) (S + vv) : 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 9; ++j) {
+            const uint32_t idx = 64u * j + lane, f = idx / 9u, k = idx - 9u * f;
+            dga[j] = shfl_u64(A16, f) + 16u * k;
+            dlim[j] = __shfl(lim, (int) f) - (int32_t) (16u * k);
+            dlow |= (k < 4u ? 1u : 0u) << j;
+        }
+        dma(0u); // window 1's covers
+    };
     CallState c0{};
     if (threadIdx.x == 0) {
         c0.epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         c0.ticket = use_ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
         c0.nbase = DEC ? 0ull : nonce_base(ctl);
     }
-    if (!mem && !use_ticket)
-        fetch(blockIdx.x);
+    if (!use_ticket) {
+        if (mem) {
+            fetch_mem(blockIdx.x);
+            mem_start();
+        } else {
+            fetch(blockIdx.x);
+        }
+        publish_steps();
+    }
     if (threadIdx.x == 0)
         sh_cs = c0;
     __syncthreads();
     const CallState cs = sh_cs;
     const uint32_t epoch = cs.epoch;
     const uint32_t wg = use_ticket ? cs.ticket : blockIdx.x;
-    if (!mem && use_ticket)
-        fetch(wg);
+    if (use_ticket) {
+        if (mem) {
+            fetch_mem(wg);
+            mem_start();
+        } else {
+            fetch(wg);
+        }
+        publish_steps();
+        __syncthreads();
+    }
+    uint32_t KS = 0; // super-steps of the workgroup
+#pragma unroll
+    for (uint32_t k = 0; k < 2 * kFramesWaves; ++k)
+        KS = sh_steps[k] > KS ? sh_steps[k] : KS;
+    KS = __builtin_amdgcn_readfirstlane((KS + 1u) >> 1);
+    const uint32_t stw = __builtin_amdgcn_readfirstlane(sh_steps[wv]); // this pair's windows (provisional)
+    ST_STAMP(1u);
     const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -231,41 +344,12 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
     const bool is_big = valid && !small && S > 0;
     if (!small)
         S = 0;
-    // compute waves hand the frame's stream addresses and length to their
-    // memory wave through the frame's overflow slots (first written in
-    // super-step 0's second window, after barrier B_0)
-    if (!mem) {
-        uint32_t nwc = (S + 63u) >> 6;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const uint32_t o = __shfl_xor(nwc, d);
-            nwc = o > nwc ? o : nwc;
-        }
-        if (lane == 0)
-            sh_steps[wv] = nwc;
-        unsigned long long *const ho = (unsigned long long *) (myring + 256u);
-        ho[0] = A;
-        ho[1] = B;
-        ho[2] = S;
-    }
-    __syncthreads();
-    if (mem) {
-        const unsigned long long *const ho = (const unsigned long long *) (myring + 256u);
-        A = ho[0];
-        B = ho[1];
-        S = (uint32_t) ho[2];
-    }
-    uint32_t stw = 0; // this pair's windows (its longest frame)
-    uint32_t KS = 0;  // super-steps of the workgroup (every wave meets every barrier)
-#pragma unroll
-    for (uint32_t k = 0; k < kFramesWaves; ++k) {
-        const uint32_t v = sh_steps[k];
-        stw = k == wv ? v : stw;
-        KS = v > KS ? v : KS;
-    }
-    stw = __builtin_amdgcn_readfirstlane(stw);
-    KS = __builtin_amdgcn_readfirstlane((KS + 1u) >> 1);
-    const uint32_t nw = (S + 63u) >> 6;
+    // compute waves hand the frame's final stream length (decode: 0 after a
+    // failed header check) to the memory wave through overflow slot 2 (first
+    // written in super-step 2; read in super-step 0)
+    if (!mem)
+        *(uint32_t *) (myring + 288u) = S;
+    uint32_t nw = (S + 63u) >> 6;
     const uint32_t va = (uint32_t) A & 15u; // input phase: stream byte 0 at cover byte va
     const uint32_t ub = (uint32_t) B & 15u; // output phase: output byte q = ub + stream byte
     const uint32_t u4 = ub & 3u, up = u4 ? u4 : 4u;
@@ -277,61 +361,42 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
     if (mem) {
         // ================================================================ memory wave
         const uint32_t lo = DEC ? 33u : 32u; // first stream byte of the ring-stored output
+        const uint64_t Bg = B - ub;
         // output q ranges (q = ub + stream byte, from the 16-byte boundary
         // Bg): head [hs, he) and tail [ts, te) by this lane, whole granules
-        // [ga, gb) by the wave
-        const uint32_t te = S > lo ? ub + S : 0u, hs = ub + lo;
-        const uint32_t hr = (hs + 15u) & ~15u;
-        const uint32_t he = te ? (hr < te ? hr : te) : 0u;
-        uint32_t ga = 0, gb = 0;
-        if (te && (te >> 4) > (hr >> 4)) {
-            ga = hr >> 4;
-            gb = te >> 4;
-        }
-        const uint32_t tsf = te & ~15u;
-        const uint32_t ts = te ? (tsf > he ? tsf : he) : 0u;
-        const uint64_t Bg = B - ub;
-
-        // DMA lanes: instruction j, lane -> granule k of frame f (idx = 64 j + lane = 9 f + k)
-        uint64_t dga[9];
-        int32_t dlim[9];
-        uint32_t dlow = 0; // bit j: granule k < 4 (window 0's part of super-step 0: read by its lane)
-        {
-            const uint64_t A16 = A - va;
-            const int32_t lim = S ? (int32_t) (S + va) : 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 9; ++j) {
-                const uint32_t idx = 64u * j + lane, f = idx / 9u, k = idx - 9u * f;
-                dga[j] = shfl_u64(A16, f) + 16u * k;
-                dlim[j] = __shfl(lim, (int) f) - (int32_t) (16u * k);
-                dlow |= (k < 4u ? 1u : 0u) << j;
-            }
-        }
-        auto dma = [&](uint32_t K) { // super-step K's covers -> input buffer K & 1 (no wait)
-            const uint32_t b = pl_off + (K & 1u) * kSxInBuf;
-#pragma unroll
-            for (uint32_t j = 0; j < 9; ++j)
-                if (!(ZMQG_ST_ABLATE & 2) && (int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u)))
-                    lds_dma16(dga[j] + 128ull * K, b + 1024u * j);
-        };
+        // [ga, gb) by the wave; from the final S (super-step 0)
+        const uint32_t hs = ub + lo, hr = (hs + 15u) & ~15u;
+        uint32_t te = 0, he = 0, ts = 0, ga = 0, gb = 0;
         // store lanes: instruction j, lane -> granule k = lane & 7 of frame f = 8 j + lane / 8
         const uint32_t sk = lane & 7u;
         uint64_t sga[8];
         uint32_t srg[8];
         int32_t sglo[8], sghi[8];
         uint32_t smask[8][4]; // k = 0 lanes: the bytes of granule 0 that come from the overflow slot
+        auto setup_out = [&]() { // (super-step 0, after the hand-off of the final S)
+            S = *(const uint32_t *) (myring + 288u);
+            nw = (S + 63u) >> 6;
+            te = S > lo ? ub + S : 0u;
+            he = te ? (hr < te ? hr : te) : 0u;
+            if (te && (te >> 4) > (hr >> 4)) {
+                ga = hr >> 4;
+                gb = te >> 4;
+            }
+            const uint32_t tsf = te & ~15u;
+            ts = te ? (tsf > he ? tsf : he) : 0u;
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) {
-            const uint32_t f = 8u * j + (lane >> 3);
-            sga[j] = shfl_u64(Bg, f) + 16u * sk;
-            srg[j] = kSxRing * f + 16u * sk;
-            sglo[j] = __shfl((int) ga, (int) f) - (int32_t) sk;
-            sghi[j] = __shfl((int) gb, (int) f) - (int32_t) sk;
-            const uint32_t ubf = (uint32_t) __shfl((int) ub, (int) f);
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t f = 8u * j + (lane >> 3);
+                sga[j] = shfl_u64(Bg, f) + 16u * sk;
+                srg[j] = kSxRing * f + 16u * sk;
+                sglo[j] = __shfl((int) ga, (int) f) - (int32_t) sk;
+                sghi[j] = __shfl((int) gb, (int) f) - (int32_t) sk;
+                const uint32_t ubf = (uint32_t) __shfl((int) ub, (int) f);
 #pragma unroll
-            for (uint32_t d = 0; d < 4; ++d)
-                smask[j][d] = lead_mask(ubf, d);
-        }
+                for (uint32_t d = 0; d < 4; ++d)
+                    smask[j][d] = lead_mask(ubf, d);
+            }
+        };
         // super-step K's ring granules -> memory (granule 0 completed from
         // super-step K-1's overflow slot)
         auto coop = [&](uint32_t K) {
@@ -366,21 +431,26 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
             }
         };
 
-        if (KS > 0u)
-            dma(0u); // window 1's covers
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // super-step 0's covers (issued at entry)
+        ST_STAMP(2u);
 #pragma unroll 1
         for (uint32_t K = 0; K < KS; ++K) {
             __syncthreads(); // B_K: super-step K's covers are in; super-step K-1's ring is complete
+            ST_STAMP(3u + (K < 16u ? K : 16u));
+            if (K == 0u)
+                setup_out();
             if (K + 1u < KS)
                 dma(K + 1u);
             if (K > 0u)
                 coop(K - 1u);
             if (K == 1u)
                 head();
+            ST_STAMP(20u + (K < 16u ? K : 16u));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the DMA, before B_K+1
+            ST_STAMP(37u + (K < 16u ? K : 16u));
         }
         __syncthreads(); // B_KS: the last super-step's ring is complete
+        ST_STAMP(58u);
         if (KS > 0u) {
             coop(KS - 1u);
             if (KS == 1u)
@@ -403,7 +473,11 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every store of the frames drained before B_fin
+        ST_STAMP(59u);
         __syncthreads();                                 // B_fin
+        ST_STAMP(60u);
+        ST_STAMP(61u);
+        ST_RTSTAMP(63u);
         return;
     }
 
@@ -489,6 +563,7 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
         ycarry = y[15];
     }
     call_state_count(zs);
+    ST_STAMP(2u);
 
     // ---- windows 1 ..
     auto window = [&](uint32_t K, uint32_t hh) {
@@ -566,16 +641,22 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
 #pragma unroll 1
     for (uint32_t K = 0; K < KS; ++K) {
         __syncthreads(); // B_K: super-step K's covers have landed; the ring half is free
+        ST_STAMP(3u + (K < 16u ? K : 16u));
         if (K > 0u && 2u * K < stw)
             window(K, 0u);
+        ST_STAMP(20u + (K < 16u ? K : 16u));
         if (2u * K + 1u < stw)
             window(K, 1u);
+        ST_STAMP(37u + (K < 16u ? K : 16u));
     }
     __syncthreads(); // B_KS
+    ST_STAMP(58u);
     // the last window's MAC
     if (stw > 0u && nw == stw)
         poly32_window(h, pk, cp, cp_j0, cp_len);
+    ST_STAMP(59u);
     __syncthreads(); // B_fin: the memory waves' stores of these frames are done; they have left
+    ST_STAMP(60u);
 
     unsigned long long excl = 0;
     if (lb) {
@@ -629,6 +710,8 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
         if (status != 0) // (the memory wave drained its stores of this frame before B_fin)
             zero_bytes(dst, S - 33u);
     }
+    ST_STAMP(61u);
+    ST_RTSTAMP(63u);
 }
 
 } // namespace zmqg
