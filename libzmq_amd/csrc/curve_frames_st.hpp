@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
     __shared__ __attribute__((aligned(16))) uint8_t sx_lds[kFramesWaves * kSxPair];
     __shared__ unsigned long long sh_wmax[kFramesWaves];
     __shared__ CallState sh_cs;
-    __shared__ uint32_t sh_steps[kFramesWaves];
+    __shared__ uint32_t sh_steps[2 * kFramesWaves]; // per wave, both roles
     const bool lb = DEC && rp.lb_flag != nullptr;
     const bool use_ticket = lb && !rp.ordered; // (kernel-uniform)
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
