@@ -42,6 +42,21 @@
 #endif
 
 
+#ifndef ZMQG_SEQ_STORE
+#define ZMQG_SEQ_STORE 0 // k_frames_seq window stores: 0 default policy, 3 sc0 sc1 (experiments)
+#endif
+
+// one output dwordx4 of a window (the seq kernel's per-lane stores)
+__device__ __forceinline__ void seq_store4(uint64_t a, uint32_t x, uint32_t y, uint32_t z, uint32_t w)
+{
+    typedef unsigned int v4_ __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) v4_ __attribute__((aligned(4))) G4_;
+    if (ZMQG_SEQ_STORE == 3)
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(a), "v"((v4_){x, y, z, w}) : "memory");
+    else
+        *(G4_ *) (uintptr_t) a = (v4_){x, y, z, w};
+}
+
 #ifndef ZMQG_SEQ_AL64
 #define ZMQG_SEQ_AL64 1 // k_frames_seq decode: 64-byte payload chunks when every payload of a wave starts 64-byte aligned (0: off, for timing)
 #endif
@@ -196,10 +211,9 @@ __device__ __forceinline__ void frame_store(uint64_t B, uint32_t w, uint32_t S, 
         o[k] = __builtin_amdgcn_alignbyte(y[k], y[k - 1], sh);
     o[16] = __builtin_amdgcn_alignbyte(0u, y[15], sh);
     if (64u * w + 64u <= S) {
-        GU4a4 *p = (GU4a4 *) (uintptr_t) a;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            p[k] = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+            seq_store4(a + 16u * k, o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
         if (last) { // S == 64w + 64: the last `up` bytes
             GU8 *t = (GU8 *) (uintptr_t) (a + 64);
             if (up == 4u) {
@@ -1441,10 +1455,10 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_seq(
             const bool lastw = act && t + 1u == nw;
             if (__builtin_amdgcn_ballot_w64(lastw) == 0) {
                 if (act) {
-                    GU4 *const q = (GU4 *) (uintptr_t) cdst;
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        q[k] = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                        seq_store4((uint64_t) (uintptr_t) cdst + 16u * k, o[4 * k], o[4 * k + 1], o[4 * k + 2],
+                                   o[4 * k + 3]);
                 }
             } else {
                 const uint32_t P = S - 33u; // (act: S >= 64t + 1 > 33)

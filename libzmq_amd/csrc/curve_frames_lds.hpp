@@ -101,8 +101,13 @@ __device__ __forceinline__ void granule_store_part(uint64_t a, uint32_t lo, uint
 // buffer, and a buffer is only refilled a step after it was last read.
 __device__ __forceinline__ void lds_dma16(uint64_t gaddr, uint32_t lds_base)
 {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gaddr), "s"(lds_base)
-                 : "memory", "m0");
+    // M0 is the compiler's: saved and restored in the same statement
+    // (cdna_hip_programming.md section 5.7)
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gaddr), "s"(lds_base)
+                 : "memory");
 }
 
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src)

@@ -56,6 +56,16 @@
                          // writes, 8 no window reads from LDS, 16 no Salsa20, 32 no Poly1305
 #endif
 
+#ifndef ZMQG_ST_REGSTAGE
+#define ZMQG_ST_REGSTAGE 0 // 1: covers move by global_load_dwordx4 into the memory wave's registers and
+                           // ds_write_b128, instead of LDS-DMA
+#endif
+
+#ifndef ZMQG_ST_STORE
+#define ZMQG_ST_STORE 0 // cache policy of the ring-to-global stores: 0 default, 1 nt, 2 sc1 (write-through),
+                        // 3 sc0 sc1
+#endif
+
 #ifndef ZMQG_ST_MEMPRIO
 #define ZMQG_ST_MEMPRIO 2 // s_setprio of the memory waves (0: same as the compute waves)
 #endif
@@ -213,12 +223,26 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
     uint64_t dga[9];
     int32_t dlim[9];
     uint32_t dlow = 0; // bit j: granule k < 4 (window 0's part of super-step 0: read by its lane)
+    u32x4 stg[ZMQG_ST_REGSTAGE ? 9 : 1]; // (register staging) the covers in flight
     auto dma = [&](uint32_t K) { // super-step K's covers -> input buffer K & 1 (no wait)
         const uint32_t b = pl_off + (K & 1u) * kSxInBuf;
 #pragma unroll
         for (uint32_t j = 0; j < 9; ++j)
-            if (!(ZMQG_ST_ABLATE & 2) && (int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u)))
-                lds_dma16(dga[j] + 128ull * K, b + 1024u * j);
+            if (!(ZMQG_ST_ABLATE & 2) && (int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u))) {
+                if (ZMQG_ST_REGSTAGE)
+                    stg[ZMQG_ST_REGSTAGE ? j : 0] = *(const GCU4 *) (uintptr_t) (dga[j] + 128ull * K);
+                else
+                    lds_dma16(dga[j] + 128ull * K, b + 1024u * j);
+            }
+    };
+    auto land = [&](uint32_t K) { // (register staging) the covers loaded by dma(K) -> input buffer K & 1
+        if (ZMQG_ST_REGSTAGE) {
+            uint8_t *const b = pl + (K & 1u) * kSxInBuf + 16u * lane;
+#pragma unroll
+            for (uint32_t j = 0; j < 9; ++j)
+                if (!(ZMQG_ST_ABLATE & 2) && (int32_t) (128u * K) < dlim[j] && (K > 0u || !((dlow >> j) & 1u)))
+                    *(u32x4 *) (b + 1024u * j) = stg[ZMQG_ST_REGSTAGE ? j : 0];
+        }
     };
     auto mem_start = [&]() {
         const uint32_t vv = (uint32_t) A & 15u;
@@ -416,10 +440,30 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
                 }
             }
             const int32_t g = (int32_t) (8u * K);
+#if ZMQG_ST_STAMPS
+            if (K == 2u) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                ST_STAMP(55u);
+            }
+#endif
 #pragma unroll
             for (uint32_t j = 0; j < 8; ++j)
-                if (!(ZMQG_ST_ABLATE & 1) && g >= sglo[j] && g < sghi[j])
-                    *(GU4 *) (uintptr_t) (sga[j] + 128ull * K) = sv[j];
+                if (!(ZMQG_ST_ABLATE & 1) && g >= sglo[j] && g < sghi[j]) {
+                    const uint64_t a = sga[j] + 128ull * K;
+                    if (ZMQG_ST_STORE == 1)
+                        __builtin_nontemporal_store(sv[j], (GU4 *) (uintptr_t) a);
+                    else if (ZMQG_ST_STORE == 2) // (counted by the explicit vmcnt(0) waits; s_nop: data hazard)
+                        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(a), "v"(sv[j]) : "memory");
+                    else if (ZMQG_ST_STORE == 3)
+                        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(a), "v"(sv[j])
+                                     : "memory");
+                    else
+                        *(GU4 *) (uintptr_t) a = sv[j];
+                }
+#if ZMQG_ST_STAMPS
+            if (K == 2u)
+                ST_STAMP(56u);
+#endif
         };
         auto head = [&]() { // output bytes [hs, he) of granule hs / 16 (super-step 0, k >= 2)
             if (__builtin_amdgcn_ballot_w64(he > hs) != 0) {
@@ -431,6 +475,7 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
             }
         };
 
+        land(0u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // super-step 0's covers (issued at entry)
         ST_STAMP(2u);
 #pragma unroll 1
@@ -441,11 +486,15 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
                 setup_out();
             if (K + 1u < KS)
                 dma(K + 1u);
+            if (K == 3u)
+                ST_STAMP(54u);
             if (K > 0u)
                 coop(K - 1u);
             if (K == 1u)
                 head();
             ST_STAMP(20u + (K < 16u ? K : 16u));
+            if (K + 1u < KS)
+                land(K + 1u);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the DMA, before B_K+1
             ST_STAMP(37u + (K < 16u ? K : 16u));
         }
@@ -577,6 +626,8 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
             for (int m = 0; m < 17; ++m)
                 d[m] = (ZMQG_ST_ABLATE & 8) ? key[m & 7] + t * 0x9e3779b9u + (uint32_t) m : p[m];
         }
+        if (K == 3u && hh == 0u)
+            ST_STAMP(54u);
         uint32_t ks[16];
         if (ZMQG_ST_ABLATE & 16) {
 #pragma unroll
@@ -610,6 +661,8 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
             if (pv && !full)
                 poly32_window(h, pk, cp, cp_j0, cp_len);
         }
+        if (K == 3u && hh == 0u)
+            ST_STAMP(55u);
         uint32_t x[16];
         const uint32_t sa = va & 3u;
 #pragma unroll
@@ -633,8 +686,12 @@ __global__ __launch_bounds__(kSxThreads) void k_frames_st(
             cp[k] = DEC ? x[k] : y[k];
         cp_j0 = 0;
         cp_len = act ? (S - 64u * t < 64u ? S - 64u * t : 64u) : 0u;
+        if (K == 3u && hh == 0u)
+            ST_STAMP(56u);
         if (act)
             ring_put(K, hh, y, ycarry);
+        if (K == 3u && hh == 0u)
+            ST_STAMP(57u);
         ycarry = y[15];
     };
 

@@ -1781,20 +1781,24 @@ struct ProfSpan {
     }
 };
 
-// Frame-kernel variant: one lane per frame once the batch gives every SIMD
-// a wave -- k_frames_lds (8: LDS-staged, coalesced traffic) when more than
-// one wave per SIMD is resident, k_frames_seq (0) at exactly one, where its
-// own loads and stores measured 4 % faster -- else G lanes per frame
-// (k_frames) so that a smaller batch still spreads over the chip.  Measured
-// per launch: 65,536 x 1 KiB seq 64 / lds 67 us;
-// 131,072 x 1 KiB seq 148-155 / lds 125-137 us; 262,144 x 1 KiB seq 293-328
-// / lds 264-276 us; 1 Mi x 256 B seq 382-469 / lds 363-429 us.
-// ZMQG_FRAMES_G (0, 1, 2, 4, 8) forces a variant (experiments, tests).
+// Frame-kernel variant, from the batch size in units of the device's wave
+// slots (slots = CUs x 4 SIMDs x 64 lanes: one wave per SIMD; 65,536 on
+// MI355X).  Every variant is VALU-bound at one wave per SIMD, so the
+// choice is about spreading the keystream work evenly over the SIMDs:
+//   n <  slots/2      G = 4 lanes per frame (k_frames)
+//   n <  2 slots/3    G = 2
+//   n <= 3 slots/2    k_frames_seq (0), one lane per frame
+//   beyond            k_frames_lds (8), LDS-staged coalesced traffic
+// The thresholds are the measured crossovers of the 1 KiB sweep in
+// DESIGN.md section 3 (32,768 ... 131,072 frames, every variant forced).
+// ZMQG_FRAMES_G (0, 1, 2, 4, 8, 16) forces a variant (experiments, tests).
 int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 {
     if (ctx->force_g >= 0)
         return ctx->force_g;
-    return n > 65536u ? 8 : n >= 65536u ? 0 : n >= 32768u ? 2 : 4;
+    const uint64_t slots = 256ull * (uint64_t) (ctx->cus > 0 ? ctx->cus : 256);
+    const uint64_t n2 = 2ull * n, n3 = 3ull * n;
+    return n2 < slots ? 4 : n3 < 2 * slots ? 2 : n2 <= 3 * slots ? 0 : 8;
 }
 
 // Workgroups of the decode frame kernel the device holds at once (occupancy

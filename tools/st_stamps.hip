@@ -124,6 +124,17 @@ int main()
                     break;
                 printf("  %2d: %8lld %8lld %8lld  wait %6lld\n", K, med(a), med(m), med(b), med(wt));
             }
+            // K = 3 detail (compute: window 6 -- 54 before the keystream (LDS reads issued),
+            // 55 after keystream + MAC, 56 after the XOR, 57 after the ring writes;
+            // memory: 54 after the DMA issue, 55 (super-group 2's) LDS reads landed, 56 stores issued)
+            {
+                std::vector<long long> v[4];
+                for (size_t w : ws)
+                    for (int q = 0; q < 4; ++q)
+                        if (c[64 * w + 54 + q])
+                            v[q].push_back(at(w, 54 + q) - at(w, 6));
+                printf("  K=3 detail since B_3: %lld %lld %lld %lld\n", med(v[0]), med(v[1]), med(v[2]), med(v[3]));
+            }
             std::vector<long long> dur, clk;
             for (size_t w : ws) {
                 dur.push_back(at(w, 61));
