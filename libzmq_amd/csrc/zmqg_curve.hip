@@ -101,13 +101,13 @@ struct __attribute__((aligned(16))) FrameHot { // needed to start a chunk (96 B)
 static_assert(sizeof(FrameHot) == 96, "FrameHot layout");
 constexpr uint32_t kHotMove = 0x80; // decode in place: payload moved from wire offset 33 to 0 by k_post
 
-constexpr int kPowInline = 4; // r^(8*2^k) for k < 4 kept in the record (frames up to 17 chunks)
-struct __attribute__((aligned(16))) FramePow { // chunk factor inputs (112 B)
+constexpr int kPowInline = 6; // r^(8*2^k) for k < 6 kept in the record: a tile's in-segment powers (< 64 chunks)
+struct __attribute__((aligned(16))) FramePow { // chunk factor inputs (144 B)
     uint32_t rb[5];                // r^(Poly1305 blocks in the last chunk)
     uint32_t t[kPowInline][5];     // r^(8*2^k)
-    uint32_t pad[3];
+    uint32_t pad[1];
 };
-static_assert(sizeof(FramePow) == 112, "FramePow layout");
+static_assert(sizeof(FramePow) == 144, "FramePow layout");
 
 struct __attribute__((aligned(16))) FrameFin { // tag / status inputs (64 B)
     uint32_t hh[5];     // head blocks' Horner value times r^(body blocks)
@@ -508,29 +508,29 @@ __device__ __forceinline__ bool wave_segment_sum(uint32_t key, uint64_t v[5])
     return key != kIdle && (lane == 0 || kp != key);
 }
 
-// Combine a segment total into the frame's accumulator.  Returns true when
+// Combine one wave's share of a frame (`mine` of its nch body chunks, worth
+// `sum` at the frame's end) into the frame's accumulator.  Returns true when
 // this call completes the frame; `sum` then holds the frame total.
-__device__ __forceinline__ bool frame_combine(uint32_t g0, uint32_t nch, unsigned long long *acc, uint32_t *cnt,
+__device__ __forceinline__ bool frame_combine(uint32_t nch, uint32_t mine, unsigned long long *acc, uint32_t *cnt,
                                               uint64_t sum[5])
 {
-    const uint32_t w0 = g0 >> 6, w1 = (g0 + nch - 1) >> 6;
-    if (w0 == w1)
-        return true; // the whole frame is inside this wave's segment
-    // No fences: the partial sums and the arrival counter are agent-scope
+    if (mine == nch)
+        return true; // the whole frame went through this wave
+    // No fences: the partial sums and the chunk counter are agent-scope
     // atomics, performed at the one coherence point every XCD's atomics to
     // an address go through.  Each wave's adds have returned before its
-    // counter add issues, so the wave whose counter add returns last finds
-    // every partial in acc, and reads them back with atomic adds of zero.
-    // (An acq_rel counter add here -- buffer_wbl2 of the XCD's L2 per tile
-    // -- made frames spanning tiles 5x slower.)
+    // counter add issues, so the wave whose counter add completes the count
+    // finds every partial in acc, and reads them back with atomic adds of
+    // zero.  (An acq_rel counter add here -- buffer_wbl2 of the XCD's L2 --
+    // made frames spanning tiles 5x slower in round 1.)
     unsigned long long ret[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q)
         ret[q] = __hip_atomic_fetch_add(acc + q, (unsigned long long) sum[q], __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(ret[0]), "v"(ret[1]), "v"(ret[2]), "v"(ret[3]), "v"(ret[4]) : "memory");
-    const uint32_t old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old != w1 - w0)
+    const uint32_t old = __hip_atomic_fetch_add(cnt, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + mine != nch)
         return false;
 #pragma unroll
     for (int q = 0; q < 5; ++q)
@@ -1053,9 +1053,9 @@ __device__ __forceinline__ uint32_t byte_mask_below(int e, int k) // bytes [4k, 
 // raw granules so that nothing here becomes a private-memory copy.
 struct TileRecords {
     u32x4 h[6]; // FrameHot
-    u32x4 p[7]; // FramePow
+    u32x4 p[9]; // FramePow
 };
-static_assert(sizeof(FrameHot) == 6 * 16 && sizeof(FramePow) == 7 * 16, "records");
+static_assert(sizeof(FrameHot) == 6 * 16 && sizeof(FramePow) == 9 * 16, "records");
 
 // Unconditional loads (an idle lane reads frame 0's records and ignores
 // them): a conditional load would need a register copy at the branch join,
@@ -1068,7 +1068,7 @@ __device__ __forceinline__ void load_records(TileRecords &R, uint32_t i, const F
     for (int q = 0; q < 6; ++q)
         R.h[q] = ph[q];
 #pragma unroll
-    for (int q = 0; q < 7; ++q)
+    for (int q = 0; q < 9; ++q)
         R.p[q] = pp[q];
 }
 
@@ -1100,17 +1100,20 @@ struct TileLane {
     uint32_t di;  // input stream byte 0 within its granule
     uint32_t cont, prevcont;
     uint64_t dst; // output stream byte 0
-    uint32_t f[5]; // r^(Poly1305 blocks after this chunk)
+    uint32_t P[5]; // r^(Poly1305 blocks of the later chunks of this chunk's frame segment in the tile)
+    uint32_t sig;  // what P was computed for: later chunks | 64 when they include the frame's last
     uint32_t k[8], n0, n1, r[5], nch, flags; // from FrameHot
     int32_t status;
     uint64_t out_base;
 };
 
 // Sets up tile lane T from its frame's records and returns the chunk's
-// input stream address (for the DMA).
+// input stream address (for the DMA).  `prev` is the wave's previous tile
+// (its segment powers are reused when the tile has the same frame layout);
+// `fresh` forces them to be computed.
 template <bool DEC>
 __device__ __forceinline__ uint64_t tile_setup(TileLane &T, const TileRecords &R, bool valid, const FrameLook &lk,
-                                               uint32_t g, const uint32_t *__restrict__ powtab)
+                                               uint32_t g, const TileLane &prev, bool fresh)
 {
     const uint32_t lane = threadIdx.x & 63;
     // every loaded granule counts as used from here on: a record word that
@@ -1120,7 +1123,7 @@ __device__ __forceinline__ uint64_t tile_setup(TileLane &T, const TileRecords &R
     for (int q = 0; q < 6; ++q)
         asm volatile("" ::"v"(R.h[q]));
 #pragma unroll
-    for (int q = 0; q < 7; ++q)
+    for (int q = 0; q < 9; ++q)
         asm volatile("" ::"v"(R.p[q]));
     // FrameHot words: key 0-7, r 8-12, nch 13, mlen 14, hl 15, n0 16, n1 17,
     // status 18, flags 19, in_base 20-21, out_base 22-23
@@ -1153,7 +1156,6 @@ __device__ __forceinline__ uint64_t tile_setup(TileLane &T, const TileRecords &R
     T.L = 0;
     T.dst = 0;
     T.di = 0;
-    fe f = fe_one();
     if (valid) {
         const uint32_t i = lk.i;
         T.key = i;
@@ -1172,34 +1174,70 @@ __device__ __forceinline__ uint64_t tile_setup(TileLane &T, const TileRecords &R
         }
         T.L = L;
         T.di = (uint32_t) (src & 15);
-        if (L > 0 && T.c + 1 < T.nch) {
-            // r^(Poly1305 blocks after this chunk) = r^blast * (r^8)^(nch-2-c)
-            // (FramePow words: rb 0-4, t[k] = r^(8*2^k) at 5+5k)
-            static_assert(kPowInline == 4, "inline powers");
-            f = rec_fe<0>(R.p);
-            const uint32_t m = T.nch - 2 - T.c;
-            if (m & 1)
-                fe_mul(f, rec_fe<5>(R.p));
-            if (m & 2)
-                fe_mul(f, rec_fe<10>(R.p));
-            if (m & 4)
-                fe_mul(f, rec_fe<15>(R.p));
-            if (m & 8)
-                fe_mul(f, rec_fe<20>(R.p));
-            const uint32_t *pt = powtab + (size_t) i * kMaxPow * 5;
-            for (int k = kPowInline; (m >> k) != 0; ++k)
-                if ((m >> k) & 1)
-                    fe_mul(f, load_fe(pt + 5 * k));
-        }
     }
-#pragma unroll
-    for (int q = 0; q < 5; ++q)
-        T.f[q] = f.l[q];
     const uint32_t kn = __shfl_down(T.key, 1);
     T.Ln = __shfl_down(T.L, 1);
     T.cont = (lane < 63 && T.key != kIdle && kn == T.key && T.L == kChunk && T.Ln > 0) ? 1u : 0u;
     T.prevcont = (__shfl_up(T.cont, 1) != 0 && lane > 0) ? 1u : 0u;
+
+    // Segment power: the lanes of one frame in this tile form a segment
+    // [first, e]; lane l's Horner value is worth r^(Poly1305 blocks of chunks
+    // l+1 .. e) at the segment's end: 8 per chunk, the frame's last chunk
+    // blast (FramePow.rb).  A wave inside one frame keeps the same powers
+    // tile after tile, so they are computed only when the layout changes.
+    const uint32_t kp = __shfl_up(T.key, 1);
+    const uint64_t bnd = __ballot(T.key == kIdle || lane == 0 || kp != T.key);
+    const uint64_t above = lane == 63 ? 0ull : (bnd >> (lane + 1)) << (lane + 1);
+    const uint32_t e = above ? (uint32_t) __builtin_ctzll(above) - 1u : 63u;
+    uint32_t sig = kIdle;
+    if (T.key != kIdle) {
+        const bool last = T.c + (e - lane) + 1 == T.nch && e > lane; // the segment's last chunk ends the frame
+        sig = (e - lane - (last ? 1u : 0u)) | (last ? 64u : 0u);
+    }
+    T.sig = sig;
+    if (fresh || __any(sig != prev.sig || T.key != prev.key)) {
+        // FramePow words: rb 0-4, t[k] = r^(8*2^k) at 5+5k
+        static_assert(kPowInline == 6, "segment powers use r^(8*2^k), k < 6");
+        fe P = fe_one();
+        if (sig != kIdle) {
+            if (sig & 64)
+                P = rec_fe<0>(R.p);
+            if (sig & 1)
+                fe_mul(P, rec_fe<5>(R.p));
+            if (sig & 2)
+                fe_mul(P, rec_fe<10>(R.p));
+            if (sig & 4)
+                fe_mul(P, rec_fe<15>(R.p));
+            if (sig & 8)
+                fe_mul(P, rec_fe<20>(R.p));
+            if (sig & 16)
+                fe_mul(P, rec_fe<25>(R.p));
+            if (sig & 32)
+                fe_mul(P, rec_fe<30>(R.p));
+        }
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            T.P[q] = P.l[q];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            T.P[q] = prev.P[q];
+    }
     return src;
+}
+
+// r^(Poly1305 blocks after chunk c of list frame p) = r^blast * (r^8)^(nch-2-c)
+// (c < nch - 1), from the frame's records.
+__device__ fe frame_after_power(const FramePow *__restrict__ pw, const uint32_t *__restrict__ powtab, uint32_t p,
+                                uint32_t nch, uint32_t c)
+{
+    const uint32_t *P = (const uint32_t *) (pw + p);
+    fe f = load_fe(P);
+    const uint32_t m = nch - 2 - c;
+    for (int k = 0; (m >> k) != 0; ++k)
+        if ((m >> k) & 1)
+            fe_mul(f, load_fe(k < kPowInline ? P + 5 + 5 * k : powtab + (size_t) p * kMaxPow * 5 + 5 * k));
+    return f;
 }
 
 // Chunk parameters of the cooperative rounds: in round k lane l moves
@@ -1433,13 +1471,19 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         const FrameLook lk = window_find(window_load(chunk_end, n, lo), lo, n, g);
         TileRecords R;
         load_records(R, g < total ? lk.i : 0, hot, pw);
-        const uint64_t src = tile_setup<DEC>(cur, R, g < total, lk, g, powtab);
+        const uint64_t src = tile_setup<DEC>(cur, R, g < total, lk, g, cur, true);
         tile_dma(wlds, src, cur.L);
         if (tb + 1 < te) {
             const uint32_t lo1 = next_tile_lo(lk, 64 * (tb + 1));
             lkn = window_find(window_load(chunk_end, n, lo1), lo1, n, 64 * (tb + 1) + lane);
         }
     }
+
+    // The open segment of the last tile (a frame that goes on into the next
+    // tile): its value at its end, its frame, the chunks of it this wave has
+    // processed.  Lane 0 of the next tile starts its Horner from it.
+    fe cfe = fe_zero();
+    uint32_t carry_key = kIdle, carry_cnt = 0;
 
 #pragma unroll 1
     for (uint32_t t = tb; t < te; ++t) {
@@ -1479,7 +1523,8 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         uint32_t *outw = (uint32_t *) (myslot + (dO & ~3u));
         const fe r = load_fe(cur.r);
         const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
-        fe h = fe_zero();
+        const bool cin = carry_key != kIdle && __builtin_amdgcn_readfirstlane(cur.key) == carry_key;
+        fe h = cin && lane == 0 ? cfe : fe_zero();
         uint32_t d[17];
         uint32_t carry = 0;
         if (nwin) {
@@ -1541,19 +1586,17 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         // (on the wave's last tile this sets up an all-idle tile: no DMA)
         TileLane nx;
         {
-            const uint64_t nsrc = tile_setup<DEC>(nx, Rn, has_next && gn < total, lkn, gn, powtab);
+            const uint64_t nsrc = tile_setup<DEC>(nx, Rn, has_next && gn < total, lkn, gn, cur, false);
             tile_dma(nb, nsrc, nx.L);
         }
         const FrameLook lk2 = window_find(ce2, lo2, n, 64 * (t + 2) + lane);
         ZSTAMP(3);
         if (nwin > 1)
             window(1);
-        if (L > 0) {
-            fe_mul(h, load_fe(cur.f));
+        fe_mul(h, load_fe(cur.P)); // (0 on idle lanes)
 #pragma unroll
-            for (int q = 0; q < 5; ++q)
-                v[q] = h.l[q];
-        }
+        for (int q = 0; q < 5; ++q)
+            v[q] = h.l[q];
         wave_lds_fence();
         ZSTAMP(4);
         // ---- store: coalesced interior granules, then this lane's edges
@@ -1592,9 +1635,50 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             asm volatile("" ::"v"(Fq[q])); // (see tile_setup: keep every loaded word's register)
-        if (ZMQG_ABLATE != 4 && wave_segment_sum(cur.key, v)) {
+        // Per frame segment of the tile (its sum on its first lane): a segment
+        // that ends its frame is combined (or is the whole frame); the open
+        // one goes on as the carry, or, on the wave's last tile, is moved to
+        // the frame's end and combined.
+        const bool first = ZMQG_ABLATE != 4 && wave_segment_sum(cur.key, v);
+        uint32_t mine = 0, ce = 0;
+        bool ends = false;
+        {
+            const uint32_t kp = __shfl_up(cur.key, 1);
+            const uint64_t bnd = __ballot(cur.key == kIdle || lane == 0 || kp != cur.key);
+            const uint64_t above = lane == 63 ? 0ull : (bnd >> (lane + 1)) << (lane + 1);
+            const uint32_t e = above ? (uint32_t) __builtin_ctzll(above) - 1u : 63u;
+            if (first) {
+                mine = e - lane + 1 + (lane == 0 && cin ? carry_cnt : 0u);
+                ce = cur.c + (e - lane);
+                ends = ce + 1 == cur.nch;
+            }
+        }
+        const bool open = first && !ends;
+        const uint64_t ob = __ballot(open);
+        carry_key = kIdle;
+        if (ob) {
+            const int fo = (int) __builtin_ctzll(ob);
+            const fe S = fe_from_wide(v);
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                cfe.l[q] = (uint32_t) __shfl((int) S.l[q], fo);
+            carry_key = (uint32_t) __shfl((int) cur.key, fo);
+            carry_cnt = (uint32_t) __shfl((int) mine, fo);
+        }
+        bool done = false;
+        if (first && ends) {
+            done = frame_combine(cur.nch, mine, acc + (size_t) cur.key * 5, cnt + cur.key, v);
+        } else if (open && t + 1 == te) {
+            fe S = fe_from_wide(v);
+            fe_mul(S, frame_after_power(pw, powtab, cur.key, cur.nch, ce));
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                v[q] = S.l[q];
+            done = frame_combine(cur.nch, mine, acc + (size_t) cur.key * 5, cnt + cur.key, v);
+        }
+        {
             const uint32_t p = cur.key; // list position
-            if (frame_combine(cur.g0, cur.nch, acc + (size_t) p * 5, cnt + p, v)) {
+            if (done) {
                 // FrameFin words: hh 0-4, s 5-8, tag 9-12, wire_len 13, frame 14
                 const fe hh = rec_fe<0>(Fq);
                 const uint32_t fs[4] = {rec_word<5>(Fq), rec_word<6>(Fq), rec_word<7>(Fq), rec_word<8>(Fq)};

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Kernel timing probe (experiments): times encode/decode body kernels and
+"""Kernel timing probe (experiments): times encode/decode frame kernels (and
+the chunked body kernel, when the frames are above 4.5 KiB) and
 whole calls with the ctx profiling hooks.  ZMQG_CURVE_LIB selects a build.
 Outputs are not checked (ablation builds compute garbage on purpose)."""
 import argparse
@@ -62,8 +63,10 @@ torch.cuda.synchronize()
 t1 = time.perf_counter()
 r = {"tag": a.tag, "msgs": n, "size": P, "step_us": (t1 - t0) / a.iters * 1e6}
 for name, ctx, k in [("enc_body_us", enc, 0), ("dec_body_us", dec, 1), ("enc_call_us", enc, 2),
-                     ("dec_call_us", dec, 3)]:
+                     ("dec_call_us", dec, 3), ("enc_kbody_us", enc, 4), ("dec_kbody_us", dec, 5)]:
     ms, cnt = ctx.get_profile(k)
-    r[name] = ms / max(cnt, 1) * 1e3
+    if cnt or k < 4:
+        r[name] = ms / max(cnt, 1) * 1e3
+r["gib_s"] = 2 * n * P / 2**30 / (r["step_us"] * 1e-6)
 r["ok"] = bool((st == 0).all().item()) and bool(torch.equal(back, payload))
 print(json.dumps(r), flush=True)
