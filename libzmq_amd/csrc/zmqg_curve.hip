@@ -508,6 +508,24 @@ __device__ __forceinline__ bool wave_segment_sum(uint32_t key, uint64_t v[5])
     return key != kIdle && (lane == 0 || kp != key);
 }
 
+// Sum of the lanes' contributions when the whole wave is one segment: 32-bit
+// row sums by DPP (each lane's limbs are below 2^26 + 64 -- fe_mul's output
+// -- so a row of 16 stays below 2^31), the four rows added in 64 bits.
+// Every lane gets the total.
+__device__ __forceinline__ void wave_sum_all(uint64_t v[5])
+{
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        int x = (int) (uint32_t) v[q];
+        x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true); // row_shr:1
+        x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true); // row_shr:2
+        x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true); // row_shr:4
+        x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true); // row_shr:8
+        v[q] = (uint64_t) (uint32_t) __builtin_amdgcn_readlane(x, 15) + (uint32_t) __builtin_amdgcn_readlane(x, 31) +
+               (uint32_t) __builtin_amdgcn_readlane(x, 47) + (uint32_t) __builtin_amdgcn_readlane(x, 63);
+    }
+}
+
 // Combine one wave's share of a frame (`mine` of its nch body chunks, worth
 // `sum` at the frame's end) into the frame's accumulator.  Returns true when
 // this call completes the frame; `sum` then holds the frame total.
@@ -1254,7 +1272,10 @@ struct RoundParams {
     uint32_t q[kGroup]; // granule of the chunk this lane moves
 };
 
-__device__ __forceinline__ void round_params(RoundParams &P, uint32_t k0, uint64_t addr, uint32_t L)
+// A uniform tile (64 whole chunks of one frame: chunk s at a0 + 128 s) gets
+// its parameters by arithmetic instead.
+__device__ __forceinline__ void round_params(RoundParams &P, uint32_t k0, uint64_t addr, uint32_t L, bool uni,
+                                             uint64_t a0)
 {
     uint32_t ln = threadIdx.x & 63;
     asm volatile("" : "+v"(ln)); // keep the round arithmetic out of the loop-invariant set
@@ -1263,18 +1284,33 @@ __device__ __forceinline__ void round_params(RoundParams &P, uint32_t k0, uint64
     for (uint32_t j = 0; j < kGroup; ++j) {
         const uint32_t idx = (k0 + j) * 64 + ln, s = idx / kSlotG;
         P.q[j] = idx - kSlotG * s;
-        P.a[j] = ((uint64_t) (uint32_t) __shfl(ahi, (int) s) << 32) | (uint32_t) __shfl(alo, (int) s);
-        P.L[j] = (uint32_t) __shfl(L, (int) s);
+        if (uni) {
+            P.a[j] = a0 + kChunk * s;
+            P.L[j] = kChunk;
+        } else {
+            P.a[j] = ((uint64_t) (uint32_t) __shfl(ahi, (int) s) << 32) | (uint32_t) __shfl(alo, (int) s);
+            P.L[j] = (uint32_t) __shfl(L, (int) s);
+        }
     }
 }
 
+// Whether the tile is uniform (see round_params), and its chunk 0 address.
+__device__ __forceinline__ bool tile_uniform(uint32_t key, uint32_t L, uint64_t addr, uint64_t &a0)
+{
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    // (the builtin returns int: each half is taken as uint32_t before widening)
+    a0 = ((uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (addr >> 32)) << 32) |
+         (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) addr);
+    return __all(key == k0 && k0 != kIdle && L == kChunk);
+}
+
 // Coalesced LDS-DMA of a tile's input images into buf (no wait).
-__device__ __forceinline__ void tile_dma(uint8_t *buf, uint64_t src, uint32_t L)
+__device__ __forceinline__ void tile_dma(uint8_t *buf, uint64_t src, uint32_t L, bool uni, uint64_t a0)
 {
 #pragma unroll
     for (uint32_t k0 = 0; k0 < kSlotG; k0 += kGroup) {
         RoundParams P;
-        round_params(P, k0, src, L);
+        round_params(P, k0, src, L, uni, a0);
 #pragma unroll
         for (uint32_t j = 0; j < kGroup; ++j) {
             const uint32_t off = (uint32_t) (P.a[j] & 15);
@@ -1288,12 +1324,13 @@ __device__ __forceinline__ void tile_dma(uint8_t *buf, uint64_t src, uint32_t L)
 // Coalesced stores of a tile's interior output granules from buf: the
 // whole granules of each chunk's output image (an edge granule, shared with
 // a neighbour or partial, is stored by its lane).
-__device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t dst, uint32_t L)
+__device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t dst, uint32_t L, bool uni,
+                                                    uint64_t d0)
 {
 #pragma unroll
     for (uint32_t k0 = 0; k0 < kSlotG; k0 += kGroup) {
         RoundParams P;
-        round_params(P, k0, dst, L);
+        round_params(P, k0, dst, L, uni, d0);
         u32x4 g[kGroup];
 #pragma unroll
         for (uint32_t j = 0; j < kGroup; ++j)
@@ -1472,7 +1509,9 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         TileRecords R;
         load_records(R, g < total ? lk.i : 0, hot, pw);
         const uint64_t src = tile_setup<DEC>(cur, R, g < total, lk, g, cur, true);
-        tile_dma(wlds, src, cur.L);
+        uint64_t a0;
+        const bool uni = tile_uniform(cur.key, cur.L, src, a0);
+        tile_dma(wlds, src, cur.L, uni, a0);
         if (tb + 1 < te) {
             const uint32_t lo1 = next_tile_lo(lk, 64 * (tb + 1));
             lkn = window_find(window_load(chunk_end, n, lo1), lo1, n, 64 * (tb + 1) + lane);
@@ -1587,7 +1626,10 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         TileLane nx;
         {
             const uint64_t nsrc = tile_setup<DEC>(nx, Rn, has_next && gn < total, lkn, gn, cur, false);
-            tile_dma(nb, nsrc, nx.L);
+            uint64_t a0;
+            const bool uni = tile_uniform(nx.key, nx.L, nsrc, a0);
+            if (ZMQG_ABLATE != 6) // (timing experiments only)
+                tile_dma(nb, nsrc, nx.L, uni, a0);
         }
         const FrameLook lk2 = window_find(ce2, lo2, n, 64 * (t + 2) + lane);
         ZSTAMP(3);
@@ -1601,7 +1643,11 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         ZSTAMP(4);
         // ---- store: coalesced interior granules, then this lane's edges
         if (ZMQG_ABLATE != 5) // (timing experiments only)
-            tile_store_interior(cb, cur.dst, L);
+        {
+            uint64_t d0;
+            const bool uni = tile_uniform(cur.key, L, cur.dst, d0);
+            tile_store_interior(cb, cur.dst, L, uni, d0);
+        }
         if (L > 0 && ZMQG_ABLATE != 3) {
             const uint32_t end = dO + L;
             GU8 *gbase = (GU8 *) (uintptr_t) (cur.dst - dO);
@@ -1639,7 +1685,16 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         // that ends its frame is combined (or is the whole frame); the open
         // one goes on as the carry, or, on the wave's last tile, is moved to
         // the frame's end and combined.
-        const bool first = ZMQG_ABLATE != 4 && wave_segment_sum(cur.key, v);
+        bool first = false;
+        if (ZMQG_ABLATE != 4) {
+            const uint32_t k0 = __builtin_amdgcn_readfirstlane(cur.key);
+            if (__all(cur.key == k0 && k0 != kIdle)) { // one frame's segment: plain wave sum
+                wave_sum_all(v);
+                first = lane == 0;
+            } else {
+                first = wave_segment_sum(cur.key, v);
+            }
+        }
         uint32_t mine = 0, ce = 0;
         bool ends = false;
         {
