@@ -1272,10 +1272,7 @@ struct RoundParams {
     uint32_t q[kGroup]; // granule of the chunk this lane moves
 };
 
-// A uniform tile (64 whole chunks of one frame: chunk s at a0 + 128 s) gets
-// its parameters by arithmetic instead.
-__device__ __forceinline__ void round_params(RoundParams &P, uint32_t k0, uint64_t addr, uint32_t L, bool uni,
-                                             uint64_t a0)
+__device__ __forceinline__ void round_params(RoundParams &P, uint32_t k0, uint64_t addr, uint32_t L)
 {
     uint32_t ln = threadIdx.x & 63;
     asm volatile("" : "+v"(ln)); // keep the round arithmetic out of the loop-invariant set
@@ -1284,17 +1281,75 @@ __device__ __forceinline__ void round_params(RoundParams &P, uint32_t k0, uint64
     for (uint32_t j = 0; j < kGroup; ++j) {
         const uint32_t idx = (k0 + j) * 64 + ln, s = idx / kSlotG;
         P.q[j] = idx - kSlotG * s;
-        if (uni) {
-            P.a[j] = a0 + kChunk * s;
-            P.L[j] = kChunk;
-        } else {
-            P.a[j] = ((uint64_t) (uint32_t) __shfl(ahi, (int) s) << 32) | (uint32_t) __shfl(alo, (int) s);
-            P.L[j] = (uint32_t) __shfl(L, (int) s);
-        }
+        P.a[j] = ((uint64_t) (uint32_t) __shfl(ahi, (int) s) << 32) | (uint32_t) __shfl(alo, (int) s);
+        P.L[j] = (uint32_t) __shfl(L, (int) s);
     }
 }
 
-// Whether the tile is uniform (see round_params), and its chunk 0 address.
+// A uniform tile: 64 whole chunks of one frame, chunk s at a0 + 128 s (input
+// and output alike).  Its rounds need no per-chunk parameters: round k of
+// lane l moves granule q of chunk s, 64k + l = 9s + q, which sits 128s + 16q =
+// 16(64k + l - s) bytes after the tile's first granule -- a per-lane constant
+// (UniRounds, computed once per wave).  q = 8 is the granule past a chunk's
+// 128 bytes: it holds input only when the tile is misaligned, and on output
+// it (like q = 0 when misaligned) is an edge granule its lane stores.
+struct UniRounds {
+    uint32_t o[5]; // the offsets of rounds 2i (low half) and 2i+1 (high half)
+    uint32_t f;    // bit k: q = 8 in round k; bit 16 + k: q = 0
+};
+
+__device__ __forceinline__ UniRounds uni_rounds()
+{
+    UniRounds U = {{0, 0, 0, 0, 0}, 0};
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t k = 0; k < kSlotG; ++k) {
+        const uint32_t idx = 64 * k + lane, s = idx / kSlotG, q = idx - kSlotG * s;
+        U.o[k >> 1] |= (16 * (idx - s)) << (16 * (k & 1));
+        U.f |= (q == kSlotG - 1 ? 1u << k : 0u) | (q == 0 ? 1u << (16 + k) : 0u);
+    }
+    return U;
+}
+
+template <uint32_t K>
+__device__ __forceinline__ uint32_t uni_off(const UniRounds &U)
+{
+    return (K & 1) ? U.o[K >> 1] >> 16 : U.o[K >> 1] & 0xffffu;
+}
+
+// LDS-DMA of a uniform tile's input (a0 = chunk 0's first stream byte).
+__device__ __forceinline__ void tile_dma_uni(uint8_t *buf, uint64_t a0, const UniRounds &U)
+{
+    const uint32_t off = (uint32_t) a0 & 15u;
+    const GU8 *base = (const GU8 *) (uintptr_t) (a0 - off);
+    const bool all9 = off != 0; // (an aligned chunk's 128 bytes are 8 granules)
+#define ZMQG_UNI_DMA(K)                                                                                         \
+    if (all9 || !((U.f >> (K)) & 1u))                                                                            \
+        __builtin_amdgcn_global_load_lds((GVoid *) (base + uni_off<K>(U)), (LdsVoid *) (buf + 1024 * (K)), 16, 0, 0);
+    ZMQG_UNI_DMA(0) ZMQG_UNI_DMA(1) ZMQG_UNI_DMA(2) ZMQG_UNI_DMA(3) ZMQG_UNI_DMA(4)
+    ZMQG_UNI_DMA(5) ZMQG_UNI_DMA(6) ZMQG_UNI_DMA(7) ZMQG_UNI_DMA(8)
+#undef ZMQG_UNI_DMA
+}
+
+// Interior output granules of a uniform tile (d0 = chunk 0's first output byte).
+__device__ __forceinline__ void tile_store_uni(const uint8_t *buf, uint64_t d0, const UniRounds &U)
+{
+    const uint32_t pO = (uint32_t) d0 & 15u;
+    GU8 *base = (GU8 *) (uintptr_t) (d0 - pO);
+    const uint32_t skip = (U.f & 0x1ffu) | (pO ? U.f >> 16 : 0u); // edge granules: their lanes store them
+    const uint8_t *lb = buf + 16 * (threadIdx.x & 63);
+#define ZMQG_UNI_ST(K)                                                 \
+    {                                                                   \
+        const u32x4 g = *(const u32x4 *) (lb + 1024 * (K));             \
+        if (!((skip >> (K)) & 1u))                                      \
+            *(GU4 *) (base + uni_off<K>(U)) = g;                        \
+    }
+    ZMQG_UNI_ST(0) ZMQG_UNI_ST(1) ZMQG_UNI_ST(2) ZMQG_UNI_ST(3) ZMQG_UNI_ST(4)
+    ZMQG_UNI_ST(5) ZMQG_UNI_ST(6) ZMQG_UNI_ST(7) ZMQG_UNI_ST(8)
+#undef ZMQG_UNI_ST
+}
+
+// Whether the tile is uniform, and its chunk 0 address.
 __device__ __forceinline__ bool tile_uniform(uint32_t key, uint32_t L, uint64_t addr, uint64_t &a0)
 {
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
@@ -1305,12 +1360,12 @@ __device__ __forceinline__ bool tile_uniform(uint32_t key, uint32_t L, uint64_t 
 }
 
 // Coalesced LDS-DMA of a tile's input images into buf (no wait).
-__device__ __forceinline__ void tile_dma(uint8_t *buf, uint64_t src, uint32_t L, bool uni, uint64_t a0)
+__device__ __forceinline__ void tile_dma(uint8_t *buf, uint64_t src, uint32_t L)
 {
 #pragma unroll
     for (uint32_t k0 = 0; k0 < kSlotG; k0 += kGroup) {
         RoundParams P;
-        round_params(P, k0, src, L, uni, a0);
+        round_params(P, k0, src, L);
 #pragma unroll
         for (uint32_t j = 0; j < kGroup; ++j) {
             const uint32_t off = (uint32_t) (P.a[j] & 15);
@@ -1324,13 +1379,12 @@ __device__ __forceinline__ void tile_dma(uint8_t *buf, uint64_t src, uint32_t L,
 // Coalesced stores of a tile's interior output granules from buf: the
 // whole granules of each chunk's output image (an edge granule, shared with
 // a neighbour or partial, is stored by its lane).
-__device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t dst, uint32_t L, bool uni,
-                                                    uint64_t d0)
+__device__ __forceinline__ void tile_store_interior(const uint8_t *buf, uint64_t dst, uint32_t L)
 {
 #pragma unroll
     for (uint32_t k0 = 0; k0 < kSlotG; k0 += kGroup) {
         RoundParams P;
-        round_params(P, k0, dst, L, uni, d0);
+        round_params(P, k0, dst, L);
         u32x4 g[kGroup];
 #pragma unroll
         for (uint32_t j = 0; j < kGroup; ++j)
@@ -1486,7 +1540,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
     const unsigned long long *__restrict__ psnap, PostOp *__restrict__ post)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kBufLds];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint8_t *const wlds = lds + wv * 2 * kBufLds;
     // the frame kernel before this one advanced the epoch: its list is parity epoch-1
     const unsigned long long lc = zs->list_ctr[(zs->epoch - 1u) & 1u];
@@ -1498,6 +1552,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
     const uint32_t tb = (uint32_t) (tiles * W / NW), te = (uint32_t) (tiles * (W + 1) / NW);
     if (tb < te) {
 
+    const UniRounds U = uni_rounds();
     // prologue: locate tile tb from scratch, set it up and start its DMA;
     // locate tile tb+1
     TileLane cur;
@@ -1510,8 +1565,10 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         load_records(R, g < total ? lk.i : 0, hot, pw);
         const uint64_t src = tile_setup<DEC>(cur, R, g < total, lk, g, cur, true);
         uint64_t a0;
-        const bool uni = tile_uniform(cur.key, cur.L, src, a0);
-        tile_dma(wlds, src, cur.L, uni, a0);
+        if (tile_uniform(cur.key, cur.L, src, a0))
+            tile_dma_uni(wlds, a0, U);
+        else
+            tile_dma(wlds, src, cur.L);
         if (tb + 1 < te) {
             const uint32_t lo1 = next_tile_lo(lk, 64 * (tb + 1));
             lkn = window_find(window_load(chunk_end, n, lo1), lo1, n, 64 * (tb + 1) + lane);
@@ -1628,8 +1685,12 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
             const uint64_t nsrc = tile_setup<DEC>(nx, Rn, has_next && gn < total, lkn, gn, cur, false);
             uint64_t a0;
             const bool uni = tile_uniform(nx.key, nx.L, nsrc, a0);
-            if (ZMQG_ABLATE != 6) // (timing experiments only)
-                tile_dma(nb, nsrc, nx.L, uni, a0);
+            if (ZMQG_ABLATE == 6) { // (timing experiments only)
+            } else if (uni) {
+                tile_dma_uni(nb, a0, U);
+            } else {
+                tile_dma(nb, nsrc, nx.L);
+            }
         }
         const FrameLook lk2 = window_find(ce2, lo2, n, 64 * (t + 2) + lane);
         ZSTAMP(3);
@@ -1645,8 +1706,10 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         if (ZMQG_ABLATE != 5) // (timing experiments only)
         {
             uint64_t d0;
-            const bool uni = tile_uniform(cur.key, L, cur.dst, d0);
-            tile_store_interior(cb, cur.dst, L, uni, d0);
+            if (tile_uniform(cur.key, L, cur.dst, d0))
+                tile_store_uni(cb, d0, U);
+            else
+                tile_store_interior(cb, cur.dst, L);
         }
         if (L > 0 && ZMQG_ABLATE != 3) {
             const uint32_t end = dO + L;
