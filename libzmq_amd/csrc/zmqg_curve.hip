@@ -867,11 +867,27 @@ __global__ __launch_bounds__(64) void k_replay_frames(uint32_t n, uint32_t T, ui
         __builtin_amdgcn_wave_barrier();
         const bool dup = in && tag[s] != lane;
         if (__builtin_amdgcn_ballot_w64(dup) != 0) {
-            for (uint32_t d = 1; d < 64; ++d) {
-                const uint32_t sj = __shfl_up(s, d);
-                const unsigned long long vj = __shfl_up(v, d);
-                if (lane >= d && in && sj == s && vj > x)
-                    x = vj;
+            // one repeated session per round: the max over its earlier lanes
+            // (an inclusive max-scan of its lanes' values, shifted by one)
+            unsigned long long left = __builtin_amdgcn_ballot_w64(in);
+            while (left) {
+                const uint32_t lead = (uint32_t) __builtin_ctzll(left);
+                const uint32_t sl = (uint32_t) __builtin_amdgcn_readlane((int) s, (int) lead);
+                const bool mem = in && s == sl;
+                const unsigned long long m = __builtin_amdgcn_ballot_w64(mem);
+                left &= ~m;
+                if ((m & (m - 1)) == 0)
+                    continue; // one lane: nothing earlier in this group
+                unsigned long long c = mem ? v : 0ull;
+#pragma unroll
+                for (uint32_t d = 1; d < 64; d <<= 1) {
+                    const unsigned long long u = __shfl_up(c, d);
+                    if (lane >= d && u > c)
+                        c = u;
+                }
+                const unsigned long long ex = __shfl_up(c, 1);
+                if (mem && lane > 0 && ex > x)
+                    x = ex;
             }
         }
         if (ok)
@@ -2060,6 +2076,21 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
 #undef ZMQG_LAUNCH_FRAMES
 }
 
+// Frames per tile of the session tables (k_replay_*, k_nonce_*): at least
+// 256 and at least the session count (a tile's table row costs S entries,
+// so that stays below its frames' work), doubled until there are at most
+// kReplayMaxTiles tiles.  Small batches get many tiles, so the per-tile walk
+// (k_*_frames, one wave each) spreads over the chip.
+uint32_t replay_tile_frames(uint32_t nn, uint32_t S)
+{
+    uint32_t T = 256;
+    while (T < S)
+        T *= 2;
+    while ((nn + T - 1) / T > kReplayMaxTiles)
+        T *= 2;
+    return T;
+}
+
 // ZMQG_OPT_NONCE_AUTO over several sessions: each frame's nonce into w.nonce
 // (k_nonce_*), advancing the sessions' send counters, on `st` before the
 // frame kernel.
@@ -2067,9 +2098,7 @@ int nonce_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st)
 {
     Workspace &w = ctx->ws;
     const uint32_t S = ctx->max_sessions;
-    uint32_t T = 4096;
-    while ((nn + T - 1) / T > kReplayMaxTiles)
-        T *= 2;
+    const uint32_t T = replay_tile_frames(nn, S);
     const uint32_t tiles = (nn + T - 1) / T, rbs = (tiles + kReplayRB - 1) / kReplayRB;
     const size_t need = ((size_t) tiles + rbs + 1) * S; // tables, block sums, send snapshot
     if (need > w.rt_cap) {
@@ -2104,9 +2133,7 @@ int replay_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st
     Workspace &w = ctx->ws;
     const uint32_t S = ctx->max_sessions;
     if (S <= kReplayMaxSessions) {
-        uint32_t T = 4096;
-        while ((nn + T - 1) / T > kReplayMaxTiles)
-            T *= 2;
+        const uint32_t T = replay_tile_frames(nn, S);
         const uint32_t tiles = (nn + T - 1) / T, rbs = (tiles + kReplayRB - 1) / kReplayRB;
         const size_t need = ((size_t) tiles + rbs + 1) * S; // tables, block sums, send snapshot
         if (need > w.rt_cap) {
