@@ -155,10 +155,11 @@ def main():
     for _ in range(args.warmup):
         step(stream)
     torch.cuda.synchronize(dev)
-    # correctness of the work being timed
-    assert int((st_out != 0).sum()) == 0, "decode failures in warmup"
-    assert torch.equal(back, payload), "round trip mismatch"
-    assert torch.equal(fl_out.cpu(), torch.from_numpy(flags_np)), "flags mismatch"
+    # correctness of the work being timed (the timed steps are checked again below)
+    if args.warmup > 0:
+        assert int((st_out != 0).sum()) == 0, "decode failures in warmup"
+        assert torch.equal(back, payload), "round trip mismatch"
+        assert torch.equal(fl_out.cpu(), torch.from_numpy(flags_np)), "flags mismatch"
 
     # The K timed steps are captured once as a hipGraph (the kernels' per-call
     # state lives on the device, so replays are exact) and replayed as one
