@@ -388,6 +388,52 @@ __device__ __forceinline__ void poly32_window_full(Poly32 &h, const PolyKey32 &k
         poly32_block(h, c[4 * j], c[4 * j + 1], c[4 * j + 2], c[4 * j + 3], 1u, k);
 }
 
+// Conversions between the two forms (the chunked path's Horner runs in radix
+// 2^32, its cross-lane sums in 26-bit limbs).  r: a clamped key's limbs.
+__device__ __forceinline__ PolyKey32 poly32_key_from_fe(const uint32_t r[5])
+{
+    return poly32_key(r[0] | (r[1] << 26), (r[1] >> 6) | (r[2] << 20), (r[2] >> 12) | (r[3] << 14),
+                      (r[3] >> 18) | (r[4] << 8));
+}
+
+// A partially reduced element (limbs a little above 2^26 allowed) as h0..h4
+// (h4 small: the value is below 2^131).
+__device__ __forceinline__ Poly32 fe_to_poly32(fe x)
+{
+    uint32_t c;
+    c = x.l[0] >> 26;
+    x.l[0] &= M26;
+    x.l[1] += c;
+    c = x.l[1] >> 26;
+    x.l[1] &= M26;
+    x.l[2] += c;
+    c = x.l[2] >> 26;
+    x.l[2] &= M26;
+    x.l[3] += c;
+    c = x.l[3] >> 26;
+    x.l[3] &= M26;
+    x.l[4] += c; // < 2^26 + 2: h4 <= 4
+    Poly32 h;
+    h.h0 = x.l[0] | (x.l[1] << 26);
+    h.h1 = (x.l[1] >> 6) | (x.l[2] << 20);
+    h.h2 = (x.l[2] >> 12) | (x.l[3] << 14);
+    h.h3 = (x.l[3] >> 18) | (x.l[4] << 8);
+    h.h4 = x.l[4] >> 24;
+    return h;
+}
+
+// h (h4 <= 6) as 26-bit limbs, the top one below 2^27 (fe_mul's input bound).
+__device__ __forceinline__ fe poly32_to_fe(const Poly32 &h)
+{
+    fe x;
+    x.l[0] = h.h0 & M26;
+    x.l[1] = ((h.h0 >> 26) | (h.h1 << 6)) & M26;
+    x.l[2] = ((h.h1 >> 20) | (h.h2 << 12)) & M26;
+    x.l[3] = ((h.h2 >> 14) | (h.h3 << 18)) & M26;
+    x.l[4] = (h.h3 >> 8) | (h.h4 << 24);
+    return x;
+}
+
 // Tag = (h mod 2^130-5) + s mod 2^128 (h4 <= 4, so one conditional
 // subtraction of p reduces it).
 __device__ __forceinline__ void poly32_finish(const Poly32 &h, const uint32_t s[4], uint32_t tag[4])

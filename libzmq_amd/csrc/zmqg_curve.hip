@@ -1633,10 +1633,11 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         uint8_t *const myslot = cb + lane * kSlot;
         const uint32_t *inw = (const uint32_t *) (myslot + (cur.di & ~3u));
         uint32_t *outw = (uint32_t *) (myslot + (dO & ~3u));
-        const fe r = load_fe(cur.r);
-        const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+        // the chunk's Horner in radix 2^32 (poly32_*: 0.75x the radix-2^26
+        // instructions per block), back in 26-bit limbs for the segment sums
+        const PolyKey32 pk = poly32_key_from_fe(cur.r);
         const bool cin = carry_key != kIdle && __builtin_amdgcn_readfirstlane(cur.key) == carry_key;
-        fe h = cin && lane == 0 ? cfe : fe_zero();
+        Poly32 h = fe_to_poly32(cin && lane == 0 ? cfe : fe_zero());
         uint32_t d[17];
         uint32_t carry = 0;
         if (nwin) {
@@ -1660,16 +1661,16 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
             salsa20_block(ks, cur.k, cur.n0, cur.n1, 1 + 2 * cur.c + tw, 0);
 #endif
             if (DEC && ZMQG_ABLATE != 2)
-                poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+                poly32_window(h, pk, w, 0u, (uint32_t) nv);
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 w[q] ^= ks[q];
             if (nv < 64)
                 mask_tail(w, nv);
             if (!DEC && ZMQG_ABLATE != 2)
-                poly_absorb64(h, r, s1, s2, s3, s4, w, nv);
+                poly32_window(h, pk, w, 0u, (uint32_t) nv);
 #if ZMQG_ABLATE == 2
-            h.l[0] ^= w[0];
+            h.h0 ^= w[0];
 #endif
             if (tw + 1 < nwin) { // read ahead before this window's output overwrites it
 #pragma unroll
@@ -1712,10 +1713,11 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         ZSTAMP(3);
         if (nwin > 1)
             window(1);
-        fe_mul(h, load_fe(cur.P)); // (0 on idle lanes)
+        fe hf = poly32_to_fe(h);
+        fe_mul(hf, load_fe(cur.P)); // (0 on idle lanes)
 #pragma unroll
         for (int q = 0; q < 5; ++q)
-            v[q] = h.l[q];
+            v[q] = hf.l[q];
         wave_lds_fence();
         ZSTAMP(4);
         // ---- store: coalesced interior granules, then this lane's edges
