@@ -1660,15 +1660,23 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
 #else
             salsa20_block(ks, cur.k, cur.n0, cur.n1, 1 + 2 * cur.c + tw, 0);
 #endif
-            if (DEC && ZMQG_ABLATE != 2)
-                poly32_window(h, pk, w, 0u, (uint32_t) nv);
+            if (DEC && ZMQG_ABLATE != 2) {
+                if (__all(nv == 64))
+                    poly32_window_full(h, pk, w);
+                else
+                    poly32_window(h, pk, w, 0u, (uint32_t) nv);
+            }
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 w[q] ^= ks[q];
             if (nv < 64)
                 mask_tail(w, nv);
-            if (!DEC && ZMQG_ABLATE != 2)
-                poly32_window(h, pk, w, 0u, (uint32_t) nv);
+            if (!DEC && ZMQG_ABLATE != 2) {
+                if (__all(nv == 64))
+                    poly32_window_full(h, pk, w);
+                else
+                    poly32_window(h, pk, w, 0u, (uint32_t) nv);
+            }
 #if ZMQG_ABLATE == 2
             h.h0 ^= w[0];
 #endif
@@ -1766,12 +1774,20 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         // that ends its frame is combined (or is the whole frame); the open
         // one goes on as the carry, or, on the wave's last tile, is moved to
         // the frame's end and combined.
-        bool first = false;
+        bool first = false, carried = false;
         if (ZMQG_ABLATE != 4) {
             const uint32_t k0 = __builtin_amdgcn_readfirstlane(cur.key);
             if (__all(cur.key == k0 && k0 != kIdle)) { // one frame's segment: plain wave sum
                 wave_sum_all(v);
-                first = lane == 0;
+                const uint32_t c0 = __builtin_amdgcn_readfirstlane(cur.c), nch = __builtin_amdgcn_readfirstlane(cur.nch);
+                if (c0 + 64 < nch && t + 1 < te) { // the frame goes on into the next tile: it is the carry
+                    cfe = fe_from_wide(v);
+                    carry_cnt = 64 + (cin ? carry_cnt : 0u);
+                    carry_key = k0;
+                    carried = true;
+                } else {
+                    first = lane == 0;
+                }
             } else {
                 first = wave_segment_sum(cur.key, v);
             }
@@ -1791,7 +1807,8 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         }
         const bool open = first && !ends;
         const uint64_t ob = __ballot(open);
-        carry_key = kIdle;
+        if (!carried)
+            carry_key = kIdle;
         if (ob) {
             const int fo = (int) __builtin_ctzll(ob);
             const fe S = fe_from_wide(v);
