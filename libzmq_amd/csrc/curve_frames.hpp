@@ -1051,7 +1051,15 @@ __device__ __forceinline__ void frame_load_exact(uint64_t A4, uint32_t lim, uint
 // Same frame semantics, replay rule, big-frame hand-off and call state as
 // k_frames with G = 1.
 template <bool DEC, class BigOp>
-__global__ __launch_bounds__(kFramesBS) void k_frames_seq(
+#ifndef ZMQG_SEQ_WPE
+#define ZMQG_SEQ_WPE 0 // k_frames_seq: minimum waves per SIMD the register allocation must allow (0: no bound)
+#endif
+#if ZMQG_SEQ_WPE
+#define ZMQG_SEQ_ATTR __attribute__((amdgpu_waves_per_eu(ZMQG_SEQ_WPE)))
+#else
+#define ZMQG_SEQ_ATTR
+#endif
+__global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
     uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
     const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,

@@ -29,8 +29,8 @@ payload = torch.randint(0, 256, (n * P,), dtype=torch.uint8, device=dev)
 enc = C.CurveContext(0, a.sessions)
 dec = C.CurveContext(0, a.sessions)
 for s in range(a.sessions):
-    enc.session_set(s, bytes(range(s, s + 32)), C.CLIENT_PREFIX, C.SERVER_PREFIX)
-    dec.session_set(s, bytes(range(s, s + 32)), C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+    enc.session_set(s, bytes((s + j) % 256 for j in range(32)), C.CLIENT_PREFIX, C.SERVER_PREFIX)
+    dec.session_set(s, bytes((s + j) % 256 for j in range(32)), C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
 t = lambda x, d: torch.from_numpy(np.ascontiguousarray(x).view(d)).to(dev)
 sid = t((np.arange(n) * a.sessions // n).astype(np.uint32), np.int32)
 flags = torch.zeros(n, dtype=torch.uint8, device=dev)
