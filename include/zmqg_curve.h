@@ -251,6 +251,29 @@ int zmqg_decode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
                      const uint32_t *wire_len, const uint8_t *in, uint64_t in_bytes, const uint64_t *out_off,
                      uint8_t *out, uint64_t out_bytes, uint8_t *flags_out, int32_t *status_out);
 
+/* One message on one session, host memory in and out: the call the
+ * reference engine makes per message (curve_encoding_t::encode / decode,
+ * src/curve_mechanism_base.cpp:111-205, :207-284, from
+ * src/stream_engine_base.cpp:331-348 / :281-291) without descriptor arrays.
+ * The bytes are copied once into the ctx's page-locked, device-mapped
+ * message buffer, the frame kernel works on it in place over PCIe (no
+ * hipMemcpy), and the result is copied once out of it after the stream
+ * has synchronised.
+ *
+ * zmqg_encode_msg: `out` receives zmqg_wire_size(flags, downgrade of sid,
+ * len) bytes, the MESSAGE command for `nonce`.
+ * zmqg_decode_msg: `out` receives wire_len - 33 payload bytes (`out` may be
+ * `in`: the payload then starts at in[0]; a frame shorter than 33 bytes
+ * fails its header checks and needs no room), *flags_out the
+ * plaintext MORE / COMMAND bits and *status_out 0 or the
+ * ZMQ_PROTOCOL_ERROR_ZMTP_* code; on a failure `out` is left untouched and
+ * the session's peer nonce advances as the reference's does.
+ * Both return 0 or -errno (-EINVAL for bad arguments). */
+int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, const uint8_t *in, uint32_t len,
+                    uint8_t *out);
+int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wire_len, uint8_t *out,
+                    uint8_t *flags_out, int32_t *status_out);
+
 /* Asynchronous host path.  The reference's
  * engine encodes and decodes one message at a time on the I/O thread
  * (src/stream_engine_base.cpp:281-291 in_event, :331-348 out_event); an

@@ -196,6 +196,8 @@ struct zmqg_ctx {
     // host staging for the *_host entry points
     uint8_t *pin = nullptr;
     size_t pin_bytes = 0;
+    uint8_t *mpin = nullptr, *mpin_dev = nullptr; // the per-message buffer (zmqg_*_msg), device-mapped
+    size_t mpin_bytes = 0;
     uint8_t *dbuf = nullptr;
     size_t dbuf_bytes = 0;
     hipStream_t own_stream = nullptr;
@@ -2285,6 +2287,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     }
     if (ctx->pin)
         (void) hipHostFree(ctx->pin);
+    if (ctx->mpin)
+        (void) hipHostFree(ctx->mpin);
     if (ctx->own_stream)
         (void) hipStreamDestroy(ctx->own_stream);
     for (auto &v : ctx->prof)
@@ -2754,6 +2758,101 @@ int zmqg_encode_host(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     ZCHECK(ctx, hipMemcpyAsync(h + o_out, d + o_out, out_bytes, hipMemcpyDeviceToHost, st));
     ZCHECK(ctx, hipStreamSynchronize(st));
     memcpy(out, h + o_out, out_bytes);
+    return 0;
+}
+
+// The per-message buffer: page-locked and device-mapped, the kernels read the
+// message and write the result in place.
+static int msg_stage(zmqg_ctx *ctx, size_t bytes)
+{
+    if (bytes <= ctx->mpin_bytes)
+        return 0;
+    size_t cap = ctx->mpin_bytes ? ctx->mpin_bytes : 65536;
+    while (cap < bytes)
+        cap *= 2;
+    if (ctx->mpin)
+        ZCHECK(ctx, hipHostFree(ctx->mpin));
+    ctx->mpin = nullptr;
+    ctx->mpin_bytes = 0;
+    hipError_t e = hipHostMalloc((void **) &ctx->mpin, cap, hipHostMallocMapped | hipHostMallocPortable);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+        return -ENOMEM;
+    ZCHECK(ctx, e);
+    void *d = nullptr;
+    ZCHECK(ctx, hipHostGetDevicePointer(&d, ctx->mpin, 0));
+    ctx->mpin_dev = (uint8_t *) d;
+    ctx->mpin_bytes = cap;
+    return 0;
+}
+
+// descriptors of the one message: sid, len, nonce / in_off, out_off, flags
+struct MsgDesc {
+    uint32_t sid, len;
+    uint64_t nonce, in_off, out_off;
+    uint8_t flags, flags_out, pad[2];
+    int32_t status;
+};
+
+int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, const uint8_t *in, uint32_t len,
+                    uint8_t *out)
+{
+    if (!ctx || (len && !in) || !out)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (sid >= ctx->max_sessions)
+        return -EINVAL;
+    const uint64_t W = zmqg_wire_size(flags, ctx->h_downgrade[sid], len);
+    const size_t o_in = al(sizeof(MsgDesc)), o_out = al(o_in + len);
+    int rc = msg_stage(ctx, o_out + W);
+    if (rc)
+        return rc;
+    MsgDesc *h = (MsgDesc *) ctx->mpin;
+    *h = MsgDesc{sid, len, nonce, 0, 0, flags, 0, {0, 0}, 0};
+    if (len)
+        memcpy(ctx->mpin + o_in, in, len);
+    uint8_t *d = ctx->mpin_dev;
+    MsgDesc *dd = (MsgDesc *) d;
+    hipStream_t st = ctx->own_stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    rc = zmqg_encode_batch(ctx, 1, &dd->sid, &dd->nonce, &dd->flags, &dd->in_off, &dd->len, d + o_in, &dd->out_off,
+                           d + o_out, st);
+    if (rc)
+        return rc;
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    memcpy(out, ctx->mpin + o_out, W);
+    return 0;
+}
+
+int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wire_len, uint8_t *out,
+                    uint8_t *flags_out, int32_t *status_out)
+{
+    if (!ctx || (wire_len && !in) || (wire_len > 33u && !out) || !flags_out || !status_out)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (sid >= ctx->max_sessions)
+        return -EINVAL;
+    const uint64_t P = wire_len >= 33u ? wire_len - 33u : 0u; // (a shorter frame fails its header checks)
+    const size_t o_in = al(sizeof(MsgDesc)), o_out = al(o_in + wire_len);
+    int rc = msg_stage(ctx, o_out + P);
+    if (rc)
+        return rc;
+    MsgDesc *h = (MsgDesc *) ctx->mpin;
+    *h = MsgDesc{sid, wire_len, 0, 0, 0, 0, 0, {0, 0}, 0};
+    if (wire_len)
+        memcpy(ctx->mpin + o_in, in, wire_len);
+    uint8_t *d = ctx->mpin_dev;
+    MsgDesc *dd = (MsgDesc *) d;
+    hipStream_t st = ctx->own_stream;
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    rc = zmqg_decode_batch(ctx, 1, &dd->sid, &dd->in_off, &dd->len, d + o_in, &dd->out_off, d + o_out,
+                           &dd->flags_out, &dd->status, st);
+    if (rc)
+        return rc;
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    *status_out = h->status;
+    *flags_out = h->status == 0 ? h->flags_out : 0;
+    if (h->status == 0 && P)
+        memcpy(out, ctx->mpin + o_out, P);
     return 0;
 }
 

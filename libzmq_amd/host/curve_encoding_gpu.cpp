@@ -121,18 +121,50 @@ curve_encoding_gpu_t::nonce_t curve_encoding_gpu_t::get_peer_nonce () const
     return p;
 }
 
-int curve_encoding_gpu_t::encode (msg_buf_t *msg_)
+int curve_encoding_gpu_t::encode_msg (const uint8_t *in_,
+                                      size_t len_,
+                                      uint8_t flags_,
+                                      uint8_t *out_)
 {
-    curve_encoding_gpu_t *e = this;
-    return encode_many (&e, &msg_, 1);
+    if (len_ > 0xffffffffu) {
+        errno = EINVAL;
+        return -1;
+    }
+    if (sync_session () != 0) {
+        errno = EIO;
+        return -1;
+    }
+    const nonce_t nonce = get_and_inc_nonce (); // src/curve_mechanism_base.cpp:114-116
+    const int rc =
+      zmqg_encode_msg (_ctx, _sid, nonce, flags_, in_, (uint32_t) len_, out_);
+    if (rc != 0) {
+        errno = -rc;
+        return -1;
+    }
+    return 0;
 }
 
-int curve_encoding_gpu_t::decode (msg_buf_t *msg_, int *error_event_code_)
+int curve_encoding_gpu_t::decode_msg (const uint8_t *in_,
+                                      size_t wire_len_,
+                                      uint8_t *out_,
+                                      uint8_t *flags_out_,
+                                      int *error_event_code_)
 {
-    curve_encoding_gpu_t *d = this;
-    int32_t status = 0;
-    if (decode_many (&d, &msg_, 1, &status) != 0)
+    if (wire_len_ > 0xffffffffu) {
+        errno = EINVAL;
         return -1;
+    }
+    if (sync_session () != 0) {
+        errno = EIO;
+        return -1;
+    }
+    int32_t status = 0;
+    const int rc = zmqg_decode_msg (_ctx, _sid, in_, (uint32_t) wire_len_, out_,
+                                    flags_out_, &status);
+    if (rc != 0) {
+        errno = -rc;
+        return -1;
+    }
     if (status != 0) {
         //  src/curve_mechanism_base.cpp:84-108, 277-281
         if (error_event_code_)
@@ -140,6 +172,29 @@ int curve_encoding_gpu_t::decode (msg_buf_t *msg_, int *error_event_code_)
         errno = EPROTO;
         return -1;
     }
+    return 0;
+}
+
+int curve_encoding_gpu_t::encode (msg_buf_t *msg_)
+{
+    std::vector<uint8_t> wire (wire_size (msg_->flags, msg_->size ()));
+    if (encode_msg (msg_->data (), msg_->size (), msg_->flags, &wire[0]) != 0)
+        return -1;
+    msg_->bytes.swap (wire);
+    msg_->flags = 0; // the boxed message is a fresh msg_t
+    return 0;
+}
+
+int curve_encoding_gpu_t::decode (msg_buf_t *msg_, int *error_event_code_)
+{
+    const size_t w = msg_->size ();
+    uint8_t fl = 0;
+    //  decoded in place: the payload lands at the front of the wire bytes
+    if (decode_msg (msg_->data (), w, msg_->data (), &fl, error_event_code_)
+        != 0)
+        return -1;
+    msg_->bytes.resize (w - 33);
+    msg_->flags |= fl; // msg_t::set_flags ORs (src/msg.cpp:433-436)
     return 0;
 }
 

@@ -89,6 +89,23 @@ class curve_encoding_gpu_t
     //  payload and the plaintext MORE/COMMAND bits are ORed into its flags.
     int decode (msg_buf_t *msg_, int *error_event_code_);
 
+    //  The same on raw bytes, one message per device call with no
+    //  intermediate buffers (zmqg_encode_msg / zmqg_decode_msg): encode_msg
+    //  writes wire_size (flags_, len_) bytes to out_; decode_msg writes the
+    //  wire_len_ - 33 payload bytes to out_ (which may be in_) and sets
+    //  *flags_out_ to the plaintext MORE / COMMAND bits.  The MESSAGE path
+    //  of zmq::curve_encoding_t (zmq_curve_encoding.hpp).
+    size_t wire_size (uint8_t flags_, size_t len_) const
+    {
+        return zmqg_wire_size (flags_, _downgrade_sub ? 1 : 0, len_);
+    }
+    int encode_msg (const uint8_t *in_, size_t len_, uint8_t flags_, uint8_t *out_);
+    int decode_msg (const uint8_t *in_,
+                    size_t wire_len_,
+                    uint8_t *out_,
+                    uint8_t *flags_out_,
+                    int *error_event_code_);
+
     //  Batched forms: one device submission for all messages, each message on
     //  its own connection's session.  Return 0, or -1 with errno set when the
     //  call itself failed; per-message results of decode_many are in

@@ -69,16 +69,17 @@ class curve_encoding_t
             errno = EPROTO;
             return -1;
         }
-        zmqg::msg_buf_t m;
-        const uint8_t *p = static_cast<const uint8_t *> (msg_->data ());
-        m.bytes.assign (p, p + msg_->size ());
-        m.flags = msg_->flags (); //  more / command / subscribe / cancel
-        if (_gpu.encode (&m) == -1)
-            return -1;
+        //  more / command / subscribe / cancel
+        const uint8_t fl = static_cast<uint8_t> (msg_->flags ());
         msg_t box;
-        int rc = box.init_size (m.size ());
+        int rc = box.init_size (_gpu.wire_size (fl, msg_->size ()));
         errno_assert (rc == 0);
-        memcpy (box.data (), m.data (), m.size ());
+        //  the device writes the box straight from the message's bytes
+        if (_gpu.encode_msg (static_cast<const uint8_t *> (msg_->data ()),
+                             msg_->size (), fl,
+                             static_cast<uint8_t *> (box.data ()))
+            == -1)
+            return -1;
         rc = msg_->move (box);
         errno_assert (rc == 0);
         return 0;
@@ -100,15 +101,15 @@ class curve_encoding_t
             errno = EPROTO;
             return -1;
         }
-        zmqg::msg_buf_t m;
-        const uint8_t *p = static_cast<const uint8_t *> (msg_->data ());
-        m.bytes.assign (p, p + msg_->size ());
-        if (_gpu.decode (&m, error_event_code_) == -1)
+        //  decoded in place: the payload lands at the front of the
+        //  message, which is then shrunk to it (:253-260)
+        uint8_t *p = static_cast<uint8_t *> (msg_->data ());
+        uint8_t fl = 0;
+        if (_gpu.decode_msg (p, msg_->size (), p, &fl, error_event_code_)
+            == -1)
             return -1;
-        if (m.size ())
-            memcpy (msg_->data (), m.data (), m.size ());
-        msg_->shrink (m.size ());
-        msg_->set_flags (m.flags);
+        msg_->shrink (msg_->size () - 33);
+        msg_->set_flags (fl);
         return 0;
     }
 
