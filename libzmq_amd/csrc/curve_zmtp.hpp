@@ -118,32 +118,6 @@ constexpr uint32_t kZmtpWgBytes = 64u * kZmtpThreads;    // 16 KiB of stream per
 constexpr uint32_t kZmtpWgCap = kZmtpWgBytes / 8u;         // candidates a workgroup can hold
 constexpr unsigned long long kZmtpNone = ~0ull;
 
-// exclusive sum over the workgroup's threads (256); total to every thread
-__device__ __forceinline__ uint32_t zmtp_block_excl(uint32_t v, uint32_t &total)
-{
-    __shared__ uint32_t sh[kZmtpThreads / 64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t) __shfl_up((int) x, d);
-        if ((int) lane >= d)
-            x += o;
-    }
-    if (lane == 63)
-        sh[wv] = x;
-    __syncthreads();
-    uint32_t base = 0;
-    total = 0;
-    for (uint32_t k = 0; k < kZmtpThreads / 64; ++k) {
-        if (k < wv)
-            base += sh[k];
-        total += sh[k];
-    }
-    __syncthreads();
-    return base + x - v;
-}
-
 // byte o (static) of a little-endian register window
 template <int O, int NW>
 __device__ __forceinline__ uint32_t zmtp_byte(const uint32_t (&w)[NW])
@@ -182,35 +156,65 @@ __device__ __forceinline__ uint64_t zmtp_cand_at(const uint32_t (&w)[NW], uint64
     return kZmtpNone;
 }
 
+// four 16-bit counts, one per chunk round k: exclusive sum over the
+// workgroup's threads of each, the workgroup totals to every thread
+__device__ __forceinline__ uint64_t zmtp_block_excl4(uint64_t v, uint64_t &total)
+{
+    __shared__ unsigned long long sh4[kZmtpThreads / 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(x, d);
+        if ((int) lane >= d)
+            x += o;
+    }
+    if (lane == 63)
+        sh4[wv] = x;
+    __syncthreads();
+    uint64_t base = 0;
+    total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kZmtpThreads / 64; ++k) {
+        if (k < wv)
+            base += sh4[k];
+        total += sh4[k];
+    }
+    return base + x - v;
+}
+
 __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, uint64_t n, int64_t max_msg,
                                                             uint64_t *cand_wg, uint64_t *count_wg)
 {
-    // Chunk r of the workgroup (16 bytes, r = 256 k + thread): consecutive
-    // lanes read consecutive chunks (coalesced), with the 16 bytes before the
-    // chunk (a header) and the 8 after (a signature's tail), so the signature
-    // and header tests run on registers.  Candidates go out in chunk order: a
-    // block scan of the counts per k.
+    // Chunk (k, thread) = stream bytes [wg0 + 16 (256 k + thread), +16), k =
+    // 0..3: consecutive lanes read consecutive chunks (coalesced), each with
+    // the 16 bytes before it (a header) and the 8 after (a signature's tail),
+    // so the signature and header tests run on registers.  All four rounds'
+    // loads go out first; candidates go out in (k, thread) order, which is
+    // stream order, after one block scan of the four rounds' counts packed in
+    // 16-bit fields (a workgroup holds at most kZmtpWgCap = 2048 of them).
+    constexpr uint32_t R = kZmtpWgBytes / 16u / kZmtpThreads; // 4 rounds
+    static_assert(R == 4, "four 16-bit count fields");
     const uint64_t wg0 = (uint64_t) blockIdx.x * kZmtpWgBytes;
-    uint32_t base_out = 0;
     uint64_t *const dst0 = cand_wg + (size_t) blockIdx.x * kZmtpWgCap;
-#pragma unroll 1
-    for (uint32_t k = 0; k < kZmtpWgBytes / 16u / kZmtpThreads; ++k) {
+    uint32_t w[R][10]; // round k: stream bytes [base_k - 16, base_k + 24), zero outside [0, n)
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
         const uint64_t base = wg0 + 16ull * (k * kZmtpThreads + threadIdx.x);
-        uint32_t w[10]; // stream bytes [base - 16, base + 24), zero outside [0, n)
         if (base >= 16 && base + 24 <= n) {
             const uint4 v0 = *(const uint4 *) (b + base - 16);
             const uint4 v1 = *(const uint4 *) (b + base);
             const uint2 v2 = *(const uint2 *) (b + base + 16);
-            w[0] = v0.x;
-            w[1] = v0.y;
-            w[2] = v0.z;
-            w[3] = v0.w;
-            w[4] = v1.x;
-            w[5] = v1.y;
-            w[6] = v1.z;
-            w[7] = v1.w;
-            w[8] = v2.x;
-            w[9] = v2.y;
+            w[k][0] = v0.x;
+            w[k][1] = v0.y;
+            w[k][2] = v0.z;
+            w[k][3] = v0.w;
+            w[k][4] = v1.x;
+            w[k][5] = v1.y;
+            w[k][6] = v1.z;
+            w[k][7] = v1.w;
+            w[k][8] = v2.x;
+            w[k][9] = v2.y;
         } else {
 #pragma unroll
             for (int q = 0; q < 10; ++q) {
@@ -219,25 +223,32 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
                     const int64_t p = (int64_t) base - 16 + 4 * q + j;
                     x |= (uint32_t) (p >= 0 && (uint64_t) p < n ? b[p] : 0u) << (8 * j);
                 }
-                w[q] = x;
+                w[k][q] = x;
             }
         }
-        uint64_t f0 = 0, f1 = 0; // (at most 2: signatures are >= 8 bytes apart)
-        uint32_t cnt = 0;
+    }
+    uint64_t f[R][2]; // (at most 2 per chunk: signatures are >= 8 bytes apart)
+    uint32_t cnt[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+        const uint64_t base = wg0 + 16ull * (k * kZmtpThreads + threadIdx.x);
+        uint64_t f0 = 0, f1 = 0;
+        uint32_t c = 0;
         auto at = [&](uint64_t p) { // (registers only: no dynamically indexed array)
-            if (p != kZmtpNone && cnt < 2u) {
-                f1 = cnt ? p : f1;
-                f0 = cnt ? f0 : p;
-                ++cnt;
+            if (p != kZmtpNone && c < 2u) {
+                f1 = c ? p : f1;
+                f0 = c ? f0 : p;
+                ++c;
             }
         };
+        const uint32_t(&wk)[10] = w[k];
 #define ZMTP_SIG(Q, J)                                                                                           \
-    if (__builtin_amdgcn_alignbyte(w[5 + Q], w[4 + Q], J) == 0x53454d07u &&                                      \
-        __builtin_amdgcn_alignbyte(w[6 + Q], w[5 + Q], J) == 0x45474153u && base + 4 * Q + J + 8 <= n)           \
-        at(zmtp_cand_at<16 + 4 * Q + J>(w, base + 4 * Q + J, n, max_msg));
+    if (__builtin_amdgcn_alignbyte(wk[5 + Q], wk[4 + Q], J) == 0x53454d07u &&                                    \
+        __builtin_amdgcn_alignbyte(wk[6 + Q], wk[5 + Q], J) == 0x45474153u && base + 4 * Q + J + 8 <= n)         \
+        at(zmtp_cand_at<16 + 4 * Q + J>(wk, base + 4 * Q + J, n, max_msg));
 #define ZMTP_WORD(Q)                                                                                             \
     {                                                                                                            \
-        const uint32_t x = w[4 + Q] ^ 0x07070707u;                                                               \
+        const uint32_t x = wk[4 + Q] ^ 0x07070707u;                                                              \
         if ((x - 0x01010101u) & ~x & 0x80808080u) { /* a 0x07 byte in this word */                              \
             ZMTP_SIG(Q, 0)                                                                                       \
             ZMTP_SIG(Q, 1)                                                                                       \
@@ -251,13 +262,25 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
         ZMTP_WORD(3)
 #undef ZMTP_WORD
 #undef ZMTP_SIG
-        uint32_t total;
-        const uint32_t off = zmtp_block_excl(cnt, total);
-        if (cnt > 0u)
-            dst0[base_out + off] = f0;
-        if (cnt > 1u)
-            dst0[base_out + off + 1] = f1;
-        base_out += total;
+        f[k][0] = f0;
+        f[k][1] = f1;
+        cnt[k] = c;
+    }
+    uint64_t packed = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k)
+        packed |= (uint64_t) cnt[k] << (16 * k);
+    uint64_t tot;
+    const uint64_t ex = zmtp_block_excl4(packed, tot);
+    uint32_t base_out = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+        const uint32_t off = base_out + (uint32_t) ((ex >> (16 * k)) & 0xffffu);
+        if (cnt[k] > 0u)
+            dst0[off] = f[k][0];
+        if (cnt[k] > 1u)
+            dst0[off + 1] = f[k][1];
+        base_out += (uint32_t) ((tot >> (16 * k)) & 0xffffu);
     }
     if (threadIdx.x == 0)
         count_wg[blockIdx.x] = base_out;

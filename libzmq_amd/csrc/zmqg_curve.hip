@@ -2814,8 +2814,13 @@ int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, 
     MsgDesc *dd = (MsgDesc *) d;
     hipStream_t st = ctx->own_stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    rc = zmqg_encode_batch(ctx, 1, &dd->sid, &dd->nonce, &dd->flags, &dd->in_off, &dd->len, d + o_in, &dd->out_off,
-                           d + o_out, st);
+    // the frame's length bounds the batch: a frame within the frame kernel's
+    // range is one launch, with no large-frame launches behind it
+    zmqg_batch_opts o{};
+    o.size = sizeof o;
+    o.max_len = len ? len : 1u;
+    rc = zmqg_encode_batch_ex(ctx, 1, &dd->sid, &dd->nonce, &dd->flags, &dd->in_off, &dd->len, d + o_in,
+                              &dd->out_off, d + o_out, &o, st);
     if (rc)
         return rc;
     ZCHECK(ctx, hipStreamSynchronize(st));
@@ -2844,8 +2849,11 @@ int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wir
     MsgDesc *dd = (MsgDesc *) d;
     hipStream_t st = ctx->own_stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    rc = zmqg_decode_batch(ctx, 1, &dd->sid, &dd->in_off, &dd->len, d + o_in, &dd->out_off, d + o_out,
-                           &dd->flags_out, &dd->status, st);
+    zmqg_batch_opts o{};
+    o.size = sizeof o;
+    o.max_len = wire_len ? wire_len : 1u;
+    rc = zmqg_decode_batch_ex(ctx, 1, &dd->sid, &dd->in_off, &dd->len, d + o_in, &dd->out_off, d + o_out,
+                              &dd->flags_out, &dd->status, &o, st);
     if (rc)
         return rc;
     ZCHECK(ctx, hipStreamSynchronize(st));
