@@ -76,6 +76,8 @@ _lib.zmqg_decode_batch_ex.argtypes = [_P, _U64] + [_P] * 8 + [ctypes.POINTER(Bat
 _lib.zmqg_session_max_batch.argtypes = [_P, _U64] + [_P] * 6
 _lib.zmqg_encode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _U64, _P, _P, _U64]
 _lib.zmqg_decode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _U64, _P, _P, _U64, _P, _P]
+_lib.zmqg_encode_msg.argtypes = [_P, _U32, _U64, ctypes.c_uint8, _P, _U32, _P]
+_lib.zmqg_decode_msg.argtypes = [_P, _U32, _P, _U32, _P, _P, _P]
 class ZmtpResult(ctypes.Structure):  # zmqg_zmtp_result
     _fields_ = [("frames", _U64), ("consumed", _U64), ("out_bytes", _U64), ("error", ctypes.c_int32),
                 ("pad", ctypes.c_int32)]
@@ -353,6 +355,28 @@ class CurveContext:
                                           inp.nbytes, _ptr(out_off), _ptr(out), out.nbytes, _ptr(fl), _ptr(st)),
                     "zmqg_decode_host")
         return out[:out_size], fl[:n], st[:n]
+
+
+    # ---- one message, host bytes (zmqg_encode_msg / zmqg_decode_msg) ----
+    def encode_msg(self, sid, nonce, flags, payload):
+        """The MESSAGE command for one message (bytes) on session sid."""
+        p = np.frombuffer(bytes(payload), np.uint8)
+        out = np.zeros(wire_size(flags, 1 if self.downgrade[sid] else 0, len(p)), np.uint8)
+        self._check(_lib.zmqg_encode_msg(self._ctx, sid, nonce, flags, _ptr(p) if len(p) else None, len(p),
+                                         _ptr(out)), "zmqg_encode_msg")
+        return out.tobytes()
+
+    def decode_msg(self, sid, wire):
+        """(payload bytes or None, flags, status) of one received frame."""
+        w = np.frombuffer(bytes(wire), np.uint8)
+        out = np.zeros(max(len(w) - 33, 1), np.uint8)
+        fl = np.zeros(1, np.uint8)
+        st = np.zeros(1, np.int32)
+        self._check(_lib.zmqg_decode_msg(self._ctx, sid, _ptr(w) if len(w) else None, len(w), _ptr(out), _ptr(fl),
+                                         _ptr(st)), "zmqg_decode_msg")
+        if st[0] != 0:
+            return None, 0, int(st[0])
+        return out[:len(w) - 33].tobytes(), int(fl[0]), 0
 
 
 class Msg:

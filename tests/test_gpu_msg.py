@@ -1,0 +1,120 @@
+"""GPU tests of the per-message entry points (zmqg_encode_msg /
+zmqg_decode_msg, include/zmqg_curve.h), the calls the drop-in
+zmq::curve_encoding_t makes once per message as the reference engine calls
+its codec (src/stream_engine_base.cpp:281-291, :331-348), against the CPU
+oracle (src/curve_mechanism_base.cpp:111-284 restated in oracle/):
+
+* every flag / downgrade kind and sizes 0 .. 70,000 bytes (frames on both
+  sides of the frame kernel's 4.5 KiB range), bit-exact wires;
+* a message sequence decoded one call at a time with replays, reorders,
+  tampering in every wire region, wrong-length and non-MESSAGE frames: the
+  same statuses, payloads, flags and final peer nonce as the oracle's
+  sequential decode;
+* in-place decode (out == in) through the same buffer.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _sessions(C, key, downgrade=False, peer=2):
+    enc = C.CurveContext(0, 1)
+    enc.session_set(0, key, O.CLIENT_PREFIX, O.SERVER_PREFIX, downgrade)
+    dec = C.CurveContext(0, 1)
+    dec.session_set(0, key, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, peer)
+    return enc, dec
+
+
+def _oracle_wire(key, nonce, flags, payload, downgrade=False):
+    sess = O.make_sessions([key], downgrade_sub=downgrade)
+    p = np.frombuffer(payload, np.uint8) if payload else np.zeros(0, np.uint8)
+    ws = O.wire_size(flags, 1 if downgrade else 0, len(p))
+    w = O.encode_batch(sess, np.zeros(1, np.uint32), np.array([nonce], np.uint64), np.array([flags], np.uint8),
+                       np.zeros(1, np.uint64), np.array([len(p)], np.uint32), p if len(p) else np.zeros(1, np.uint8),
+                       np.zeros(1, np.uint64), ws)
+    return bytes(w[:ws])
+
+
+@pytest.mark.parametrize("downgrade", [False, True])
+def test_encode_msg_matches_oracle(torch_cuda, C, downgrade):
+    rng = np.random.default_rng(11 + downgrade)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc, _ = _sessions(C, key, downgrade)
+    nonce = 3
+    for size in (0, 1, 31, 32, 33, 34, 63, 64, 65, 1024, 4400, 4500, 4600, 70000):
+        for flags in (0, 1, 2, 3, 12, 13, 16, 17):
+            pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+            got = enc.encode_msg(0, nonce, flags, pay)
+            assert got == _oracle_wire(key, nonce, flags, pay, downgrade), (size, flags)
+            nonce += 1
+
+
+def test_decode_msg_sequence_matches_oracle(torch_cuda, C):
+    rng = np.random.default_rng(5)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc, dec = _sessions(C, key)
+    frames, nonce = [], 3
+    for size in (0, 5, 33, 1024, 5000, 70000):
+        for flags in (0, 1, 2, 3):
+            pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+            frames.append(enc.encode_msg(0, nonce, flags, pay))
+            nonce += 1
+    seq = list(frames)
+    seq.insert(3, frames[1])                     # replay
+    seq.insert(7, frames[10])                    # from the future, then its predecessors fail
+    t = bytearray(frames[12]); t[40] ^= 1        # ciphertext
+    seq.append(bytes(t))
+    t = bytearray(frames[13]); t[20] ^= 0x80     # tag
+    seq.append(bytes(t))
+    t = bytearray(frames[14]); t[1] ^= 1         # command name
+    seq.append(bytes(t))
+    seq.append(frames[15][:32])                  # too short for a MESSAGE
+    seq.append(b"")                              # empty
+    seq.append(frames[20][:-1])                  # truncated: MAC fails
+    seq.append(frames[21])
+    # oracle: the reference's sequential rule over the whole sequence
+    wl = np.array([len(w) for w in seq], np.uint32)
+    woff = np.zeros(len(seq), np.uint64)
+    pos = 0
+    for i, w in enumerate(seq):
+        woff[i] = pos
+        pos += len(w)
+    wire = np.frombuffer(b"".join(seq) + b"\0" * 64, np.uint8)
+    pout = np.zeros(len(seq), np.uint64)
+    pp = 0
+    for i, w in enumerate(seq):
+        pout[i] = pp
+        pp += max(len(w) - 33, 0)
+    sess = O.make_sessions([key], dec_prefix=O.CLIENT_PREFIX)
+    peer = np.array([2], np.uint64)
+    out, fl, st = O.decode_batch(sess, peer, np.zeros(len(seq), np.uint32), woff, wl, wire, pout, pp + 1)
+    for i, w in enumerate(seq):
+        got, gfl, gst = dec.decode_msg(0, w)
+        assert gst == int(st[i]), (i, gst, int(st[i]))
+        if gst == 0:
+            exp = bytes(out[int(pout[i]):int(pout[i]) + len(w) - 33])
+            assert got == exp and gfl == int(fl[i]), i
+    assert dec.get_peer_nonce(0) == int(peer[0])
+
+
+def test_decode_msg_in_place(torch_cuda, C):
+    """out == in: the payload lands at the front of the received bytes (the
+    drop-in's decode then shrinks the msg_t to it)."""
+    import ctypes
+    from libzmq_amd import curve as CC
+    rng = np.random.default_rng(9)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc, dec = _sessions(C, key)
+    for i, size in enumerate((0, 40, 1024, 6000)):
+        pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        w = np.frombuffer(enc.encode_msg(0, 3 + i, 1, pay), np.uint8).copy()
+        fl = np.zeros(1, np.uint8)
+        st = np.zeros(1, np.int32)
+        p = w.ctypes.data_as(ctypes.c_void_p)
+        rc = CC.lib().zmqg_decode_msg(dec._ctx, 0, p, len(w), p, fl.ctypes.data_as(ctypes.c_void_p),
+                                      st.ctypes.data_as(ctypes.c_void_p))
+        assert rc == 0 and st[0] == 0 and fl[0] == 1
+        assert w[:size].tobytes() == pay
