@@ -103,7 +103,9 @@ def main():
     if args.dry_run:
         if world > 1:
             dist.barrier()
-        print(json.dumps({"dry_run": True, "rank": rank, "local_rank": local, "world": world}), flush=True)
+        # one write(2) per line (atomic on a pipe), so the ranks' lines never interleave
+        sys.stdout.flush()
+        os.write(1, (json.dumps({"dry_run": True, "rank": rank, "local_rank": local, "world": world}) + "\n").encode())
         if world > 1:
             dist.destroy_process_group()
         return

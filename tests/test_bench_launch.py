@@ -17,7 +17,13 @@ def test_bench_gpus2_launches_two_ranks():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--msgs", "64"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(s) for s in r.stdout.splitlines() if s.startswith("{")]
+    lines, dec, pos = [], json.JSONDecoder(), 0
+    while True:  # every JSON object in the output, however the ranks' lines fell
+        pos = r.stdout.find("{", pos)
+        if pos < 0:
+            break
+        obj, pos = dec.raw_decode(r.stdout, pos)
+        lines.append(obj)
     assert sorted(d["rank"] for d in lines) == [0, 1], r.stdout
     assert all(d["world"] == 2 and d["dry_run"] for d in lines)
 
