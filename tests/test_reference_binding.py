@@ -65,8 +65,8 @@ NEEDED = [
     "zmq::msg_t::data()",
     "zmq::msg_t::size() const",
     "zmq::msg_t::flags() const",
-    "zmqg::curve_encoding_gpu_t::encode(zmqg::msg_buf_t*)",
-    "zmqg::curve_encoding_gpu_t::decode(zmqg::msg_buf_t*, int*)",
+    "zmqg::curve_encoding_gpu_t::encode_msg(unsigned char const*, unsigned long, unsigned char, unsigned char*)",
+    "zmqg::curve_encoding_gpu_t::decode_msg(unsigned char const*, unsigned long, unsigned char*, unsigned char*, int*)",
     "zmqg::acquire_session(unsigned int*)",
     "zmqg::release_session(unsigned int)",
     "zmqg::thread_ctx()",
