@@ -1,0 +1,10 @@
+#!/bin/bash
+# Config-2 kernel timings (kbench) of the default build and the variant
+# libraries given as arguments, two rounds; no parity (timing experiments).
+cd "${GRAFT_REPO_ROOT:-.}"
+for r in 1 2; do
+  timeout -k 10 120 python tools/kbench.py --iters 30 --tag default || exit 1
+  for lib in "$@"; do
+    ZMQG_CURVE_LIB=$PWD/$lib timeout -k 10 120 python tools/kbench.py --iters 30 --tag $lib || exit 1
+  done
+done
