@@ -99,7 +99,7 @@ def main():
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     if args.gpus != world:
-        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}; reporting n_gpus = {world}", file=sys.stderr)
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}; running {world} ranks", file=sys.stderr)
     if args.dry_run:
         if world > 1:
             dist.barrier()
@@ -109,10 +109,12 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    # one process per GPU; (a rehearsal with more ranks than GPUs shares them)
+    # one process per GPU; (a rehearsal with more ranks than GPUs shares them,
+    # and the line then reports the devices actually used, not the ranks)
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    n_devices, shared_devices = device_census(torch, world, local)
 
     from libzmq_amd import curve as C
 
@@ -296,7 +298,9 @@ def main():
         "value": value,
         "unit": "GiB/s",
         "msgs_per_s": total_msgs / elapsed,
-        "n_gpus": world,
+        "n_gpus": n_devices,
+        "ranks": world,
+        "shared_devices": shared_devices,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -329,6 +333,27 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def device_census(torch, world, local):
+    """(distinct physical GPUs the ranks run on, whether ranks share one).
+    Each rank names its device by host and PCI location (UUID when torch
+    exposes it); the names are gathered over the control-plane group, so a
+    rehearsal with more ranks than GPUs cannot report more GPUs than it used."""
+    import socket
+    p = torch.cuda.get_device_properties(local)
+    uuid = str(getattr(p, "uuid", "") or "")
+    pci = tuple(getattr(p, f, -1) for f in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    name = (socket.gethostname(), uuid if uuid else (pci if pci != (-1, -1, -1) else ("index", local)))
+    names = [name]
+    if world > 1:
+        import torch.distributed as dist
+        names = [None] * world
+        dist.all_gather_object(names, name)
+    n = len(set(names))
+    if world > torch.cuda.device_count():  # (one node: ranks beyond its GPUs must share)
+        n = min(n, torch.cuda.device_count())
+    return n, n < world
 
 
 def config_batches(which, rank, world):

@@ -45,7 +45,6 @@
 #include "curve_device.hpp"
 #include "curve_frames.hpp"
 #include "curve_frames_lds.hpp"
-#include "curve_frames_st.hpp"
 #include "curve_z85.hpp"
 #include "curve_x25519.hpp"
 #include "curve_zmtp.hpp"
@@ -205,7 +204,7 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
-    int frames_cap[6] = {0, 0, 0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4, seq, lds, st
+    int frames_cap[5] = {0, 0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4, seq, lds
     int force_g = -1;                 // ZMQG_FRAMES_G: frame-kernel variant override (experiments)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
@@ -2030,7 +2029,8 @@ struct ProfSpan {
 //   beyond            k_frames_lds (8), LDS-staged coalesced traffic
 // The thresholds are the measured crossovers of the 1 KiB sweep in
 // DESIGN.md section 3 (32,768 ... 131,072 frames, every variant forced).
-// ZMQG_FRAMES_G (0, 1, 2, 4, 8, 16) forces a variant (experiments, tests).
+// ZMQG_FRAMES_G (0, 1, 2, 4, 8) forces one of these variants whatever the
+// batch size, so the parity tests cover every variant the rule can pick.
 int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 {
     if (ctx->force_g >= 0)
@@ -2045,11 +2045,10 @@ int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 // MI355X_MICROARCH.md, Residency), cached per variant.
 int frames_capacity(zmqg_ctx *ctx, int G)
 {
-    int &c = ctx->frames_cap[G == 16 ? 5 : G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0 : G == 2 ? 1 : 2];
+    int &c = ctx->frames_cap[G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0 : G == 2 ? 1 : 2];
     if (c == 0) {
         int nb = 0;
-        hipError_t e = G == 16  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_st<true, DecodeHead>, kSxThreads, 0)
-                       : G == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_lds<true, DecodeHead>, kFramesBS, 0)
+        hipError_t e = G == 8   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_lds<true, DecodeHead>, kFramesBS, 0)
                        : G == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
                        : G == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
                        : G == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, kFramesBS, 0)
@@ -2066,12 +2065,6 @@ void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const
                    uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs, FrameCtl ctl)
 {
     const dim3 grid((uint32_t) (((uint64_t) n * (G == 1 || G == 2 || G == 4 ? G : 1) + kFramesBS - 1) / kFramesBS));
-    if (G == 16) {
-        hipLaunchKernelGGL((k_frames_st<DEC, BigOp>), grid, dim3(kSxThreads), 0, st, n, sid, nonce, flags, in_off, len, in,
-                           out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
-                           ctl);
-        return;
-    }
     if (G == 8) {
         hipLaunchKernelGGL((k_frames_lds<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
                            out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
@@ -2222,7 +2215,7 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
     ctx->h_downgrade.assign(max_sessions, 0);
     if (const char *fg = getenv("ZMQG_FRAMES_G")) {
         const int g = atoi(fg);
-        if (g == 0 || g == 1 || g == 2 || g == 4 || g == 8 || g == 16)
+        if (g == 0 || g == 1 || g == 2 || g == 4 || g == 8)
             ctx->force_g = g;
     }
     hipError_t e = hipSetDevice(device);
@@ -2571,9 +2564,10 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     if (!sid || !in_off || !wire_len || !in || !out_off || !out || !flags_out || !status_out)
         return -EINVAL;
     const bool verify_first = opts && (opts->flags & ZMQG_OPT_VERIFY_FIRST);
+    // (out_bytes may be 0 under VERIFY_FIRST: a batch of frames with no
+    // payload bytes -- empty or under the 33-byte minimum -- stages nothing,
+    // and each such frame still gets its own status)
     const uint64_t out_bytes = opt_out_bytes(opts);
-    if (verify_first && out_bytes == 0)
-        return -EINVAL;
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
     ctx->last_stream = st;

@@ -97,7 +97,8 @@ class curve_encoding_t
             //  rejected like a frame that fails its MAC: the mechanism emits
             //  the handshake-failed event and the engine closes this
             //  connection (src/curve_mechanism_base.cpp:38-52)
-            *error_event_code_ = ZMQG_ERR_CRYPTOGRAPHIC; //  = ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC
+            if (error_event_code_)
+                *error_event_code_ = ZMQG_ERR_CRYPTOGRAPHIC; //  = ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC
             errno = EPROTO;
             return -1;
         }

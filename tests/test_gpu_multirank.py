@@ -2,7 +2,8 @@
 127.0.0.1), each rank runs the config-2 step on its GPU -- ranks share a
 device when the box has fewer GPUs than ranks -- config 5 splits one batch
 over the ranks with shard.partition (strong scaling, sum over ranks), and
-rank 0 prints exactly one line, with n_gpus = 2 and max-over-ranks timing.
+rank 0 prints exactly one line, with n_gpus = the distinct devices used
+(1 on a one-GPU box, with shared_devices) and max-over-ranks timing.
 The multi-process path the driver's 8-GPU scaling run takes, on real
 kernels rather than the gloo tests' CPU stand-ins."""
 import json
@@ -26,7 +27,12 @@ def test_bench_two_ranks_config2_and_strong_config5():
     lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["scaling"] == "weak"
+    # n_gpus counts distinct devices: two ranks on a one-GPU box must not
+    # claim two GPUs
+    import torch
+    ndev = torch.cuda.device_count()
+    assert d["ranks"] == 2 and d["n_gpus"] == min(2, ndev) and d["shared_devices"] == (ndev < 2)
+    assert d["steps"] == 2 and d["scaling"] == "weak"
     assert d["config"]["parallelism"].startswith("frame-sharded x2")
     assert d["value"] > 0 and d["msgs_per_s"] > 0
     c5 = d["configs"]["config5"]

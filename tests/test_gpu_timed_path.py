@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 
 N, P = 65536, 1024
 W = P + 33
-VARIANTS = ["default", "0", "8", "16"]  # the library's choice, k_frames_seq, k_frames_lds, k_frames_st
+VARIANTS = ["default", "0", "8"]  # the library's choice, k_frames_seq, k_frames_lds
 
 
 def _ctx(C, variant, sessions=1):
