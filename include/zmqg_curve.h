@@ -105,6 +105,28 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx);
 int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], const uint8_t enc_prefix[16],
                      const uint8_t dec_prefix[16], int downgrade_sub, uint64_t peer_nonce);
 
+/* Install n sessions in one launch, asynchronously on `stream`: the mass
+ * handshake's counterpart of zmqg_session_set (each server connection's
+ * precom comes from crypto_box_beforenm at src/curve_server.cpp:382-383, each
+ * client's at src/curve_client_tools.hpp:105; zmqg_box_beforenm_batch
+ * derives them on the device and its k_out is passed here as is).
+ *   sid          host array: n distinct session ids below max_sessions
+ *                (-EINVAL otherwise)
+ *   precom       device-accessible, 4-byte aligned: session i's 32-byte
+ *                precomputed key at precom[32*i]
+ *   enc_prefix, dec_prefix   the 16-byte nonce prefixes, common to the batch
+ *                (one side's connections all use the same pair)
+ *   downgrade    host array of n downgrade_sub flags, or NULL (all 0)
+ *   peer_nonce   host array of n initial peer nonces, or NULL (all 1)
+ * The send nonce of each session starts at 1, as with zmqg_session_set.
+ * The host arrays are copied before the call returns; the install runs on
+ * `stream` (batch calls issued after it on that stream see the sessions),
+ * and the ctx's accessors order after it.  A second install waits for the
+ * first to have read its descriptors. */
+int zmqg_session_set_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint8_t *precom,
+                           const uint8_t enc_prefix[16], const uint8_t dec_prefix[16], const uint8_t *downgrade,
+                           const uint64_t *peer_nonce, void *stream);
+
 /* curve_encoding_t::set_peer_nonce / read back _cn_peer_nonce.  Synchronous:
  * they are ordered after the work previously issued on the stream of the
  * ctx's last batch call (no device-wide synchronisation). */

@@ -197,6 +197,11 @@ struct zmqg_ctx {
     size_t pin_bytes = 0;
     uint8_t *mpin = nullptr, *mpin_dev = nullptr; // the per-message buffer (zmqg_*_msg), device-mapped
     size_t mpin_bytes = 0;
+    // zmqg_session_set_batch: device-mapped descriptors of the last install,
+    // free again once `sinst_done` is reached
+    uint8_t *sinst = nullptr, *sinst_dev = nullptr;
+    size_t sinst_bytes = 0;
+    hipEvent_t sinst_done = nullptr;
     uint8_t *dbuf = nullptr;
     size_t dbuf_bytes = 0;
     hipStream_t own_stream = nullptr;
@@ -327,6 +332,41 @@ __global__ void k_session_setup(DevSession *tab, unsigned long long *peer, unsig
     tab[sid] = s;
     peer[sid] = ((unsigned long long) in[18] << 32) | in[17];
     send[sid] = 1; // _cn_nonce (1), src/curve_mechanism_base.cpp:59
+}
+
+// zmqg_session_set_batch: one thread per session, the two HSalsa20 subkeys
+// of k_session_setup.  `d` (device-mapped host memory): sid[n], then
+// peer_nonce[n] (u64), then downgrade[n] (u8); precom n x 32 bytes
+// (device-accessible, 4-byte aligned); pfx = enc_prefix[4] dec_prefix[4].
+struct Prefixes {
+    uint32_t w[8];
+};
+__global__ __launch_bounds__(256) void k_session_setup_batch(uint32_t n, const uint8_t *__restrict__ d,
+                                                             const uint32_t *__restrict__ precom, Prefixes pfx,
+                                                             DevSession *tab, unsigned long long *peer,
+                                                             unsigned long long *send)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t *sid = (const uint32_t *) d;
+    const unsigned long long *pn = (const unsigned long long *) (d + ((4ull * n + 7) & ~7ull));
+    const uint8_t *down = d + ((4ull * n + 7) & ~7ull) + 8ull * n;
+    const uint32_t s = sid[i];
+    uint32_t k[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        k[t] = precom[8ull * i + t];
+    DevSession x;
+    hsalsa20(x.enc_key, k, pfx.w);
+    hsalsa20(x.dec_key, k, pfx.w + 4);
+    x.downgrade_sub = down[i] ? 1u : 0u;
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+        x.pad[t] = 0;
+    tab[s] = x;
+    peer[s] = pn[i];
+    send[s] = 1; // _cn_nonce (1), src/curve_mechanism_base.cpp:59
 }
 
 __global__ void k_fill_u64(unsigned long long *p, uint32_t n, unsigned long long v)
@@ -2282,6 +2322,12 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
         (void) hipHostFree(ctx->pin);
     if (ctx->mpin)
         (void) hipHostFree(ctx->mpin);
+    if (ctx->sinst_done) {
+        (void) hipEventSynchronize(ctx->sinst_done);
+        (void) hipEventDestroy(ctx->sinst_done);
+    }
+    if (ctx->sinst)
+        (void) hipHostFree(ctx->sinst);
     if (ctx->own_stream)
         (void) hipStreamDestroy(ctx->own_stream);
     for (auto &v : ctx->prof)
@@ -2381,6 +2427,67 @@ int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], cons
         e = hipStreamSynchronize(ctx->own_stream);
     (void) hipFree(d);
     ZCHECK(ctx, e);
+    return 0;
+}
+
+int zmqg_session_set_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint8_t *precom,
+                           const uint8_t enc_prefix[16], const uint8_t dec_prefix[16], const uint8_t *downgrade,
+                           const uint64_t *peer_nonce, void *stream)
+{
+    if (!ctx || check_n(n))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!sid || !precom || ((uintptr_t) precom & 3u) || !enc_prefix || !dec_prefix)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    {
+        std::vector<uint8_t> seen(ctx->max_sessions, 0); // distinct, known sids (the install has no order)
+        for (uint64_t i = 0; i < n; ++i) {
+            if (sid[i] >= ctx->max_sessions || seen[sid[i]])
+                return -EINVAL;
+            seen[sid[i]] = 1;
+        }
+    }
+    ZCHECK(ctx, hipSetDevice(ctx->device));
+    const size_t o_peer = (4 * n + 7) & ~(size_t) 7, o_down = o_peer + 8 * n, need = o_down + n;
+    if (ctx->sinst_done)
+        ZCHECK(ctx, hipEventSynchronize(ctx->sinst_done)); // the previous install has read its descriptors
+    else
+        ZCHECK(ctx, hipEventCreateWithFlags(&ctx->sinst_done, hipEventDisableTiming));
+    if (need > ctx->sinst_bytes) {
+        if (ctx->sinst)
+            ZCHECK(ctx, hipHostFree(ctx->sinst));
+        ctx->sinst = nullptr;
+        ctx->sinst_bytes = 0;
+        hipError_t e = hipHostMalloc((void **) &ctx->sinst, need, hipHostMallocMapped | hipHostMallocPortable);
+        if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+            return -ENOMEM;
+        ZCHECK(ctx, e);
+        void *dp = nullptr;
+        ZCHECK(ctx, hipHostGetDevicePointer(&dp, ctx->sinst, 0));
+        ctx->sinst_dev = (uint8_t *) dp;
+        ctx->sinst_bytes = need;
+    }
+    memcpy(ctx->sinst, sid, 4 * n);
+    uint64_t *pn = (uint64_t *) (ctx->sinst + o_peer);
+    for (uint64_t i = 0; i < n; ++i)
+        pn[i] = peer_nonce ? peer_nonce[i] : 1u;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t dg = downgrade && downgrade[i] ? 1 : 0;
+        ctx->sinst[o_down + i] = dg;
+        ctx->h_downgrade[sid[i]] = dg;
+    }
+    Prefixes pfx;
+    memcpy(pfx.w, enc_prefix, 16);
+    memcpy(pfx.w + 4, dec_prefix, 16);
+    hipStream_t st = (hipStream_t) stream;
+    ctx->last_stream = st;
+    hipLaunchKernelGGL(k_session_setup_batch, dim3((uint32_t) ((n + 255) / 256)), dim3(256), 0, st, (uint32_t) n,
+                       (const uint8_t *) ctx->sinst_dev, (const uint32_t *) precom, pfx, ctx->sessions, ctx->peer,
+                       ctx->send);
+    ZCHECK(ctx, hipGetLastError());
+    ZCHECK(ctx, hipEventRecord(ctx->sinst_done, st));
     return 0;
 }
 

@@ -54,6 +54,7 @@ _lib.zmqg_abi_version.restype = ctypes.c_int
 _lib.zmqg_ctx_create.argtypes = [ctypes.c_int, _U32, ctypes.POINTER(_P)]
 _lib.zmqg_ctx_destroy.argtypes = [_P]
 _lib.zmqg_session_set.argtypes = [_P, _U32, _P, _P, _P, ctypes.c_int, _U64]
+_lib.zmqg_session_set_batch.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _P]
 _lib.zmqg_session_set_peer_nonce.argtypes = [_P, _U32, _U64]
 _lib.zmqg_session_get_peer_nonce.argtypes = [_P, _U32, ctypes.POINTER(_U64)]
 _lib.zmqg_session_set_nonce.argtypes = [_P, _U32, _U64]
@@ -171,6 +172,26 @@ class CurveContext:
         self.downgrade[sid] = bool(downgrade_sub)
         self._check(_lib.zmqg_session_set(self._ctx, sid, precom, enc_prefix, dec_prefix, int(bool(downgrade_sub)),
                                           peer_nonce), "zmqg_session_set")
+
+    def session_set_batch(self, sid, precom, enc_prefix, dec_prefix, downgrade=None, peer_nonce=None, stream=None):
+        """zmqg_session_set_batch: sid / downgrade / peer_nonce are host
+        sequences (numpy-convertible), precom a device tensor of n x 32 bytes
+        (e.g. box_beforenm_batch's k_out); asynchronous on `stream`."""
+        sid = np.ascontiguousarray(sid, dtype=np.uint32)
+        n = len(sid)
+        enc_prefix, dec_prefix = bytes(enc_prefix), bytes(dec_prefix)
+        if len(enc_prefix) != 16 or len(dec_prefix) != 16:
+            raise ValueError("prefixes must be 16 bytes")
+        dg = None if downgrade is None else np.ascontiguousarray(downgrade, dtype=np.uint8)
+        pn = None if peer_nonce is None else np.ascontiguousarray(peer_nonce, dtype=np.uint64)
+        if (dg is not None and len(dg) != n) or (pn is not None and len(pn) != n):
+            raise ValueError("downgrade / peer_nonce must have one entry per session")
+        self._check(_lib.zmqg_session_set_batch(self._ctx, n, sid.ctypes.data, _ptr(precom), enc_prefix, dec_prefix,
+                                                None if dg is None else dg.ctypes.data,
+                                                None if pn is None else pn.ctypes.data, _stream_handle(stream)),
+                    "zmqg_session_set_batch")
+        for i, s in enumerate(sid.tolist()):
+            self.downgrade[s] = bool(dg[i]) if dg is not None else False
 
     def set_peer_nonce(self, sid, nonce):
         self._check(_lib.zmqg_session_set_peer_nonce(self._ctx, sid, nonce), "zmqg_session_set_peer_nonce")

@@ -15,8 +15,20 @@
 //     msg_t survive, the plaintext MORE / COMMAND bits are added;
 //   * a connection that gets no session slot (ZMQG_THREAD_SESSIONS = 4, the
 //     fifth codec) fails its calls without aborting the process.
-// zmq::msg_t here is the test double in tests/host/msg_model/ (see its
-// header).  Needs a GPU; prints "OK <n>".
+//   * (ZMQG_REAL_MSG_T builds only) zero-copy receive: decode in place on a
+//     zclmsg over a shared receive buffer, as src/v2_decoder.cpp:88-113
+//     builds it (msg_t::init with an external content_t,
+//     src/msg.cpp:30-47, 108-129).
+// Two builds: tests/host/build_ref_binding.sh links the REFERENCE's own
+// msg_t (src/msg.cpp, metadata.cpp, err.cpp under /root/reference, with
+// -DZMQG_REAL_MSG_T; prints "OK 15"); tests/test_host_adapter.py also builds
+// it on the test double in tests/host/msg_model/ (prints "OK 14"), which
+// needs no reference sources.  Needs a GPU.
+#if defined ZMQG_REAL_MSG_T
+//  as every reference translation unit starts (platform.hpp, zmq.h,
+//  zmq_draft.h), before src/curve_mechanism_base.hpp would include the codec
+#include "precompiled.hpp"
+#endif
 #include "zmq_curve_encoding.hpp"
 
 #include <stdio.h>
@@ -35,6 +47,15 @@
     } while (0)
 
 static int tests_run = 0;
+
+#if defined ZMQG_REAL_MSG_T
+//  the receive buffer's free function (shared_message_memory_allocator::
+//  call_dec_ref in the reference): counts its calls
+static void zc_free (void *, void *hint_)
+{
+    ++*static_cast<int *> (hint_);
+}
+#endif
 static uint32_t key_seed = 1;
 
 static void fill (uint8_t *p, size_t n)
@@ -243,6 +264,54 @@ int main ()
             delete c[i];
         ++tests_run;
     }
+#if defined ZMQG_REAL_MSG_T
+    {   //  zero-copy receive (src/v2_decoder.cpp:88-113): each received
+        //  frame is a zclmsg whose data is the frame's place in the shared
+        //  receive buffer; decode leaves the payload there (no copy, no new
+        //  allocation, src/curve_mechanism_base.cpp:253-260) and the
+        //  buffer's free function runs once when the message closes
+        zmq::curve_encoding_t cli ("CurveZMQMESSAGEC", "CurveZMQMESSAGES",
+                                   false);
+        zmq::curve_encoding_t srv ("CurveZMQMESSAGES", "CurveZMQMESSAGEC",
+                                   false);
+        make_precoms (cli.get_writable_precom_buffer (),
+                      srv.get_writable_precom_buffer ());
+        const size_t P[3] = {200, 1, 3000}; //  boxes of 233, 34, 3033 bytes
+        std::vector<uint8_t> rx, expect[3];
+        size_t off[3], wlen[3];
+        for (int k = 0; k < 3; ++k) {
+            zmq::msg_t m;
+            CHECK (m.init_size (P[k]) == 0);
+            fill (static_cast<uint8_t *> (m.data ()), P[k]);
+            expect[k].assign (static_cast<uint8_t *> (m.data ()),
+                              static_cast<uint8_t *> (m.data ()) + P[k]);
+            m.set_flags (k == 1 ? zmq::msg_t::more : 0);
+            CHECK (cli.encode (&m) == 0);
+            off[k] = rx.size ();
+            wlen[k] = m.size ();
+            rx.insert (rx.end (), static_cast<uint8_t *> (m.data ()),
+                       static_cast<uint8_t *> (m.data ()) + m.size ());
+            CHECK (m.close () == 0);
+        }
+        srv.set_peer_nonce (0);
+        for (int k = 0; k < 3; ++k) {
+            zmq::msg_t::content_t content;
+            int frees = 0;
+            zmq::msg_t m;
+            CHECK (m.init (&rx[off[k]], wlen[k], zc_free, &frees, &content)
+                   == 0);
+            CHECK (m.is_zcmsg () && m.data () == &rx[off[k]]);
+            int ev = 0;
+            CHECK (srv.decode (&m, &ev) == 0);
+            CHECK (m.is_zcmsg () && m.data () == &rx[off[k]]);
+            CHECK (m.size () == P[k]);
+            CHECK (memcmp (&rx[off[k]], &expect[k][0], P[k]) == 0);
+            CHECK (m.flags () == (k == 1 ? zmq::msg_t::more : 0));
+            CHECK (m.close () == 0 && frees == 1);
+        }
+        ++tests_run;
+    }
+#endif
     printf ("OK %d\n", tests_run);
     return 0;
 }

@@ -126,3 +126,20 @@ def test_binding_runs_on_msg_t(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr + r.stdout
     assert r.stdout.strip() == "OK 14"
+
+
+@pytest.mark.gpu
+def test_binding_runs_on_reference_msg_t():
+    """SURVEY a10 on the REFERENCE's msg_t (src/msg.cpp:62-94 init_size,
+    305-324 move, 404-436 shrink / set_flags, 108-129 external storage),
+    prebuilt by tests/host/build_ref_binding.sh in the build step (the
+    reference is not on the GPU box): the same round trips as above plus
+    decode in place on zero-copy msg_t slices of a shared receive buffer
+    (src/v2_decoder.cpp:88-113)."""
+    exe = os.path.join(ROOT, "tests", "host", "_ref", "test_zmq_binding_ref")
+    if not os.path.exists(exe):
+        pytest.skip("tests/host/_ref/test_zmq_binding_ref not built (needs the reference sources at build time)")
+    env = dict(os.environ, ZMQG_THREAD_SESSIONS="4")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert r.stdout.strip() == "OK 15"

@@ -88,3 +88,22 @@ def test_binding_compiles_against_reference_msg_t(tmp_path):
                           check=True).stdout
     missing = [s for s in NEEDED if s not in syms]
     assert not missing, (missing, syms)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "src", "msg.cpp")),
+                    reason="reference sources not present")
+def test_binding_links_reference_msg_t():
+    """SURVEY a10 on the reference's own msg_t: tests/host/build_ref_binding.sh
+    compiles src/msg.cpp, metadata.cpp and err.cpp where they lie (test-only
+    platform.hpp) and links them with the drop-in codec and
+    tests/host/test_zmq_binding.cpp; the executable's msg_t is the reference's
+    (run on the GPU by tests/test_host_adapter.py)."""
+    r = subprocess.run(["sh", os.path.join(ROOT, "tests", "host", "build_ref_binding.sh")], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr + r.stdout
+    exe = os.path.join(ROOT, "tests", "host", "_ref", "test_zmq_binding_ref")
+    syms = subprocess.run(["nm", "-C", "--defined-only", exe], capture_output=True, text=True, check=True).stdout
+    for s in ("zmq::msg_t::init_size(unsigned long)", "zmq::msg_t::move(zmq::msg_t&)",
+              "zmq::msg_t::shrink(unsigned long)", "zmq::msg_t::set_flags(unsigned char)",
+              "zmq::msg_t::init_external_storage(", "zmq::metadata_t::drop_ref()"):
+        assert s in syms, s
