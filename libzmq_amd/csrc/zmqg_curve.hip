@@ -45,6 +45,7 @@
 #include "curve_device.hpp"
 #include "curve_frames.hpp"
 #include "curve_frames_lds.hpp"
+#include "curve_msg.hpp"
 #include "curve_z85.hpp"
 #include "curve_x25519.hpp"
 #include "curve_zmtp.hpp"
@@ -202,6 +203,7 @@ struct zmqg_ctx {
     uint8_t *sinst = nullptr, *sinst_dev = nullptr;
     size_t sinst_bytes = 0;
     hipEvent_t sinst_done = nullptr;
+    hipEvent_t order_ev = nullptr; // zmqg_*_msg: own_stream waits for the last batch stream's work
     uint8_t *dbuf = nullptr;
     size_t dbuf_bytes = 0;
     hipStream_t own_stream = nullptr;
@@ -2328,6 +2330,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     }
     if (ctx->sinst)
         (void) hipHostFree(ctx->sinst);
+    if (ctx->order_ev)
+        (void) hipEventDestroy(ctx->order_ev);
     if (ctx->own_stream)
         (void) hipStreamDestroy(ctx->own_stream);
     for (auto &v : ctx->prof)
@@ -2894,6 +2898,22 @@ struct MsgDesc {
     int32_t status;
 };
 
+// The per-message calls run on the ctx's own stream; work the ctx issued
+// before on another stream (a batch on the caller's stream) shares the
+// session tables and the workspace, so own_stream waits for it first.
+static int msg_order(zmqg_ctx *ctx)
+{
+    hipStream_t last = ctx->last_stream;
+    if (last && last != ctx->own_stream) {
+        if (!ctx->order_ev)
+            ZCHECK(ctx, hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
+        ZCHECK(ctx, hipEventRecord(ctx->order_ev, last));
+        ZCHECK(ctx, hipStreamWaitEvent(ctx->own_stream, ctx->order_ev, 0));
+    }
+    ctx->last_stream = ctx->own_stream;
+    return 0;
+}
+
 int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, const uint8_t *in, uint32_t len,
                     uint8_t *out)
 {
@@ -2915,6 +2935,18 @@ int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, 
     MsgDesc *dd = (MsgDesc *) d;
     hipStream_t st = ctx->own_stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
+    if ((rc = msg_order(ctx)))
+        return rc;
+    if (W <= kMsgMaxStream) {
+        // one wave, descriptors as arguments (curve_msg.hpp)
+        MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, nullptr, &dd->status, nonce, sid, len,
+                  ctx->max_sessions, flags};
+        hipLaunchKernelGGL(k_msg<false>, dim3(1), dim3(64), 0, st, a);
+        ZCHECK(ctx, hipGetLastError());
+        ZCHECK(ctx, hipStreamSynchronize(st));
+        memcpy(out, ctx->mpin + o_out, W);
+        return 0;
+    }
     // the frame's length bounds the batch: a frame within the frame kernel's
     // range is one launch, with no large-frame launches behind it
     zmqg_batch_opts o{};
@@ -2950,6 +2982,20 @@ int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wir
     MsgDesc *dd = (MsgDesc *) d;
     hipStream_t st = ctx->own_stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
+    if ((rc = msg_order(ctx)))
+        return rc;
+    if (wire_len <= kMsgMaxStream) {
+        MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, &dd->flags_out, &dd->status, 0, sid, wire_len,
+                  ctx->max_sessions, 0};
+        hipLaunchKernelGGL(k_msg<true>, dim3(1), dim3(64), 0, st, a);
+        ZCHECK(ctx, hipGetLastError());
+        ZCHECK(ctx, hipStreamSynchronize(st));
+        *status_out = h->status;
+        *flags_out = h->status == 0 ? h->flags_out : 0;
+        if (h->status == 0 && P)
+            memcpy(out, ctx->mpin + o_out, P);
+        return 0;
+    }
     zmqg_batch_opts o{};
     o.size = sizeof o;
     o.max_len = wire_len ? wire_len : 1u;

@@ -44,7 +44,10 @@ def test_encode_msg_matches_oracle(torch_cuda, C, downgrade):
     key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     enc, _ = _sessions(C, key, downgrade)
     nonce = 3
-    for size in (0, 1, 31, 32, 33, 34, 63, 64, 65, 1024, 4400, 4500, 4600, 70000):
+    # 4052 ... 4064: the one-wave message kernel's limit (a 4,096-byte wire
+    # frame) for every header length, on both sides
+    for size in (0, 1, 31, 32, 33, 34, 63, 64, 65, 1024, 4052, 4053, 4054, 4056, 4062, 4063, 4064, 4400, 4500,
+                 4600, 70000):
         for flags in (0, 1, 2, 3, 12, 13, 16, 17):
             pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
             got = enc.encode_msg(0, nonce, flags, pay)
@@ -57,7 +60,7 @@ def test_decode_msg_sequence_matches_oracle(torch_cuda, C):
     key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     enc, dec = _sessions(C, key)
     frames, nonce = [], 3
-    for size in (0, 5, 33, 1024, 5000, 70000):
+    for size in (0, 5, 33, 1024, 4063, 4064, 5000, 70000):
         for flags in (0, 1, 2, 3):
             pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
             frames.append(enc.encode_msg(0, nonce, flags, pay))

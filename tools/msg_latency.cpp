@@ -39,7 +39,7 @@ int main ()
     enc.get_and_inc_nonce ();
     enc.get_and_inc_nonce ();
     dec.set_peer_nonce (2);
-    const size_t sizes[] = {32, 1024, 65536, 1 << 20};
+    const size_t sizes[] = {32, 1024, 4000, 65536, 1 << 20};
     for (size_t P : sizes) {
         std::vector<uint8_t> pay (P), wire (enc.wire_size (0, P)), back (P + 64);
         for (size_t i = 0; i < P; ++i)
