@@ -15,8 +15,12 @@ barriers around the timed region (gloo, control only).
 
 JSON line fields beyond the driver contract:
   roofline      dominant kernel (decode frame kernel) achieved algorithmic HBM-read
-                GB/s vs the 8 TB/s peak, durations from HIP events recorded
-                live around that kernel on its stream during the timed steps;
+                GB/s vs the 8 TB/s peak.  HIP events cannot time a kernel
+                inside a replayed graph, so the per-launch durations come
+                from HIP events on the launch stream around each frame kernel
+                in an eager pass of K more steps run right after the timed
+                replay (the same kernels and inputs; a later stretch of the
+                GPU's power curve, DESIGN.md section 4);
                 traffic = PMC-measured HBM bytes per launch from
                 profiles/ if a PMC summary for this workload was committed;
                 valu = the same kernel against the VALU issue peak (the bound
@@ -378,6 +382,53 @@ def config_batches(which, rank, world):
     return name, np.full(hi - lo, size, np.int64), max(1, S // world), "strong"
 
 
+def config_inputs(C, torch, dev, local, rank, w, world=1):
+    """The device-resident batch and sessions of BASELINE config `w` as
+    other_configs times it (tests/test_gpu_bench_batches.py checks this exact
+    batch against the oracle): sizes from config_batches, session keys from
+    a seeded rng, payload from a seeded device generator, frames packed back
+    to back, a connection's frames together, encode nonces from each
+    session's send counter starting at 3."""
+    name, sizes, S, scaling = config_batches(w, rank, world)
+    n = len(sizes)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xC0 + 7 * rank + int(w))
+    enc, dec = C.CurveContext(local, S), C.CurveContext(local, S)
+    rng = np.random.default_rng(0xC0 + rank)
+    keys = []
+    for s in range(S):
+        k = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        keys.append(k)
+        enc.session_set(s, k, C.CLIENT_PREFIX, C.SERVER_PREFIX)
+        enc.set_nonce(s, 3)
+        dec.session_set(s, k, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+    t = lambda a, d: torch.from_numpy(np.ascontiguousarray(a).view(d)).to(dev)
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    W = sizes + 33
+    out_off = np.concatenate([[0], np.cumsum(W)[:-1]]).astype(np.uint64)
+    sid = (np.arange(n) * S // max(n, 1)).astype(np.uint32)  # a connection's frames together
+    total = int(sizes.sum())
+    ml = int(sizes.max())
+    return dict(name=name, sizes=sizes, S=S, scaling=scaling, n=n, keys=keys, enc=enc, dec=dec, sid=sid,
+                in_off=in_off, out_off=out_off, W=W, total=total,
+                d_sid=t(sid, np.int32), d_in=t(in_off, np.int64), d_out=t(out_off, np.int64),
+                d_len=t(sizes.astype(np.uint32), np.int32), d_wl=t(W.astype(np.uint32), np.int32),
+                flags=torch.zeros(n, dtype=torch.uint8, device=dev),
+                payload=torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g),
+                wire=torch.empty(int(W.sum()), dtype=torch.uint8, device=dev),
+                back=torch.empty(total, dtype=torch.uint8, device=dev),
+                fl=torch.empty(n, dtype=torch.uint8, device=dev), st=torch.empty(n, dtype=torch.int32, device=dev),
+                bound=ml if ml + 43 <= 4608 else 0)  # the frame kernel's range: skip the large-frame launches
+
+
+def config_step(b):
+    """One timed step of a config: encode with device-assigned nonces, decode."""
+    b["enc"].encode_batch(b["d_sid"], None, b["flags"], b["d_in"], b["d_len"], b["payload"], b["d_out"], b["wire"],
+                          max_len=b["bound"], nonce_auto=True)
+    b["dec"].decode_batch(b["d_sid"], b["d_out"], b["d_wl"], b["wire"], b["d_in"], b["back"], b["fl"], b["st"],
+                          max_len=b["bound"] + 33 if b["bound"] else 0)
+
+
 def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1):
     """BASELINE configs 3, 4, 5: encode (device-assigned nonces) + decode round
     trips of device-resident batches, every result checked, timed like the
@@ -387,49 +438,19 @@ def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1):
     from libzmq_amd import shard
     out = {}
     for w in which:
-        name, sizes, S, scaling = config_batches(w, rank, world)
-        n = len(sizes)
-        g = torch.Generator(device=dev)
-        g.manual_seed(0xC0 + 7 * rank + int(w))
-        enc, dec = C.CurveContext(local, S), C.CurveContext(local, S)
-        rng = np.random.default_rng(0xC0 + rank)
-        for s in range(S):
-            k = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
-            enc.session_set(s, k, C.CLIENT_PREFIX, C.SERVER_PREFIX)
-            enc.set_nonce(s, 3)
-            dec.session_set(s, k, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
-        t = lambda a, d: torch.from_numpy(np.ascontiguousarray(a).view(d)).to(dev)
-        in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
-        W = sizes + 33
-        out_off = np.concatenate([[0], np.cumsum(W)[:-1]]).astype(np.uint64)
-        sid = (np.arange(n) * S // max(n, 1)).astype(np.uint32)  # a connection's frames together
-        d_sid, d_in, d_out = t(sid, np.int32), t(in_off, np.int64), t(out_off, np.int64)
-        d_len, d_wl = t(sizes.astype(np.uint32), np.int32), t(W.astype(np.uint32), np.int32)
-        flags = torch.zeros(n, dtype=torch.uint8, device=dev)
-        total = int(sizes.sum())
-        payload = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
-        wire = torch.empty(int(W.sum()), dtype=torch.uint8, device=dev)
-        back = torch.empty(total, dtype=torch.uint8, device=dev)
-        fl = torch.empty(n, dtype=torch.uint8, device=dev)
-        st = torch.empty(n, dtype=torch.int32, device=dev)
-        ml = int(sizes.max())
-        bound = ml if ml + 43 <= 4608 else 0  # the frame kernel's range: skip the large-frame launches
-
-        def step():
-            enc.encode_batch(d_sid, None, flags, d_in, d_len, payload, d_out, wire, max_len=bound, nonce_auto=True)
-            dec.decode_batch(d_sid, d_out, d_wl, wire, d_in, back, fl, st, max_len=bound + 33 if bound else 0)
-
+        b = config_inputs(C, torch, dev, local, rank, w, world)
+        name, S, scaling, n, total = b["name"], b["S"], b["scaling"], b["n"], b["total"]
         for _ in range(warmup):
-            step()
+            config_step(b)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         for _ in range(steps):
-            step()
+            config_step(b)
         torch.cuda.synchronize(dev)
         dt = shard.max_over_ranks(time.perf_counter() - t0)
-        ok = int((st != 0).sum()) == 0 and torch.equal(back, payload)
+        ok = int((b["st"] != 0).sum()) == 0 and torch.equal(b["back"], b["payload"])
         oks = shard.max_over_ranks(0.0 if ok else 1.0) == 0.0
         assert oks, f"config {w}: round trip mismatch"
         job_bytes = total * world if scaling == "weak" else sum_over_ranks(total)
@@ -437,8 +458,9 @@ def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1):
         out["config" + w] = {"workload": name, "scaling": scaling, "value": job_bytes / 2**30 * steps / dt,
                              "unit": "GiB/s", "msgs_per_s": job_frames * steps / dt, "ms_per_step": 1e3 * dt / steps,
                              "frames_per_gpu": n, "sessions_per_gpu": S, "steps": steps, "warmup": warmup,
-                             "checked": "every frame: status 0, decoded payload == input"}
-        del payload, wire, back, enc, dec
+                             "checked": "every frame: status 0, decoded payload == input; the same batch is "
+                                        "oracle-checked by tests/test_gpu_bench_batches.py"}
+        del b
         torch.cuda.empty_cache()
     return out
 

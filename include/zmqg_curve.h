@@ -229,7 +229,11 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  *                    host memory: curve_batcher_t's receive slots).  Costs one
  *                    extra read and write of the payload bytes.
  *   out_bytes        extent of `out`: every out_off[i] + wire_len[i] - 33 is
- *                    at most this (required by ZMQG_OPT_VERIFY_FIRST).
+ *                    at most this (required by ZMQG_OPT_VERIFY_FIRST, which
+ *                    checks it on the device: a frame whose payload region
+ *                    would end past out_bytes fails with ZMQG_ERR_BOUND and
+ *                    nothing of it is written; 0 is valid for a batch whose
+ *                    frames carry no payload bytes).
  * A caller built against the struct without out_bytes passes the smaller
  * size and gets the old behaviour. */
 #define ZMQG_OPT_NONCE_AUTO 1u

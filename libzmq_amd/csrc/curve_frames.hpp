@@ -349,10 +349,24 @@ struct FrameCtl {
     PostOp *post;        // decode: header-failed frames too long for one lane to zero-fill
     uint64_t max_len;    // 0, or the caller's bound on len / wire_len
     uint32_t no_body;    // 1: no body kernel follows (every frame within max_len fits this kernel)
-    uint32_t pad;
+    uint32_t out_check;  // decode, ZMQG_OPT_VERIFY_FIRST: payload regions must end within out_limit
     unsigned long long *nonce_ctr; // encode, one session, ZMQG_OPT_NONCE_AUTO: the session's send
                                    // counter; frame i takes *nonce_ctr + i, the last workgroup adds n
+    uint64_t out_limit;  // (out_check) the caller's out_bytes: the staging area's extent
 };
+
+// A frame the call must not process (status ZMQG_ERR_BOUND, nothing
+// written): above the caller's max_len, or -- decode under
+// ZMQG_OPT_VERIFY_FIRST, whose staging area is sized from out_bytes -- a
+// payload region reaching past out_bytes.
+template <bool DEC>
+__device__ __forceinline__ bool frame_over(const FrameCtl &ctl, uint32_t L_in, uint64_t ooff)
+{
+    const bool over_len = ctl.max_len != 0 && L_in > ctl.max_len;
+    if (!DEC)
+        return over_len;
+    return over_len || (ctl.out_check && L_in > 33u && ooff + (L_in - 33u) > ctl.out_limit);
+}
 
 // Encode nonce of frame i: the caller's, or (ZMQG_OPT_NONCE_AUTO, one
 // session) the send counter read at kernel start plus i, as n calls of
@@ -565,7 +579,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     const uint8_t *src = in + in_off[ii];
     uint8_t *dst = out + out_off[ii];
     const uint32_t L_in = len[ii];
-    const bool over = ctl.max_len != 0 && L_in > ctl.max_len; // the caller's bound broken
+    const bool over = frame_over<DEC>(ctl, L_in, out_off[ii]); // the caller's bounds broken
 
     uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
     uint64_t A = 0, B = 0;
@@ -1100,7 +1114,7 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
         src = in + in_off[ii];
         dst = out + out_off[ii];
         L_in = len[ii];
-        over = ctl.max_len != 0 && L_in > ctl.max_len; // the caller's bound broken
+        over = frame_over<DEC>(ctl, L_in, out_off[ii]); // the caller's bounds broken
         if (!DEC) {
             hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
             S = sid_ok && !over ? 32u + hl + L_in : 0u;

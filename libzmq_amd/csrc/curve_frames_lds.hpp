@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     const uint8_t *src = in + in_off[ii];
     uint8_t *dst = out + out_off[ii];
     const uint32_t L_in = len[ii];
-    const bool over = ctl.max_len != 0 && L_in > ctl.max_len; // the caller's bound broken
+    const bool over = frame_over<DEC>(ctl, L_in, out_off[ii]); // the caller's bounds broken
 
     uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
     uint64_t A = 0, B = 0;

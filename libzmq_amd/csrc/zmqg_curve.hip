@@ -2710,6 +2710,10 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         ctl.no_body = opts->max_len && opts->max_len <= kMaxFrameStream;
         smax = (unsigned long long *) opts->session_max_out;
     }
+    if (verify_first) { // frames whose payload would leave the staging area fail with ZMQG_ERR_BOUND
+        ctl.out_check = 1;
+        ctl.out_limit = out_bytes;
+    }
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
     ReplayOut rp{};
     rp.vout = w.v;

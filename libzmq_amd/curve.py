@@ -248,14 +248,16 @@ class CurveContext:
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_encode_batch")
 
     def decode_batch(self, sid, in_off, wire_len, inp, out_off, out, flags_out, status_out, stream=None, max_len=0,
-                     session_max_out=None, verify_first=False):
+                     session_max_out=None, verify_first=False, out_bytes=None):
         """session_max_out: int64 tensor of max_sessions entries (device),
         receives each session's largest header-valid nonce of the batch.
         verify_first: ZMQG_OPT_VERIFY_FIRST (out receives only verified
-        payloads and zeros; out's extent is taken from the tensor)."""
+        payloads and zeros; out's extent is taken from the tensor unless
+        out_bytes is given)."""
         n = int(sid.numel())
-        o = self._opts(max_len, None, session_max_out, verify_first=verify_first,
-                       out_bytes=out.numel() * out.element_size() if verify_first else 0)
+        if out_bytes is None:
+            out_bytes = out.numel() * out.element_size() if verify_first else 0
+        o = self._opts(max_len, None, session_max_out, verify_first=verify_first, out_bytes=out_bytes)
         self._check(_lib.zmqg_decode_batch_ex(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
                                               _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_decode_batch")

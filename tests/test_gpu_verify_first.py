@@ -6,7 +6,10 @@ verifies before it decrypts (src/curve_mechanism_base.cpp:226-228).
   on batches with MAC, header and replay failures, frames on both sides of
   the frame kernel's 4.5 KiB range, separate and in-place layouts.
 * A second thread reading a pinned host `out` while forged batches are
-  decoded never sees a plaintext byte."""
+  decoded never sees a plaintext byte.
+* out_bytes = 0 is a valid extent for frames without payload bytes (each
+  gets its own status); a frame whose payload region would end past
+  out_bytes fails with ZMQG_ERR_BOUND and nothing of it is written."""
 import threading
 
 import numpy as np
@@ -125,3 +128,44 @@ def test_reader_thread_never_sees_forged_plaintext(torch_cuda, C):
           f"verify-first: {exposed_vf[0]} in {exposed_vf[1]}")
     assert exposed_vf[1] > 10
     assert exposed_vf[0] == 0
+
+
+def test_verify_first_extent_checks(torch_cuda, C):
+    torch = torch_cuda
+    rng = np.random.default_rng(91)
+    precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    # (a) no payload bytes at all: out_bytes = 0
+    sizes = [0, 0, 0]
+    wire, wire_off, wl, _ = _batch(rng, sizes, precom, tamper_every=100)
+    wl = wl.copy()
+    wl[1] = 20  # shorter than a MESSAGE
+    wl[2] = 0   # empty
+    dec = C.CurveContext(0, 1)
+    dec.session_set(0, precom, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    out = torch.full((16,), 0x77, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(3, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(3, dtype=torch.int32, device="cuda")
+    dec.decode_batch(dev(torch, np.zeros(3, np.uint32)), dev(torch, wire_off), dev(torch, wl), dev(torch, wire),
+                     dev(torch, np.zeros(3, np.uint64)), out, fl, st, verify_first=True, out_bytes=0)
+    torch.cuda.synchronize()
+    stt = host(st, np.int32)
+    assert stt[0] == 0 and stt[1] == C.ERR_MALFORMED_MESSAGE and stt[2] == C.ERR_MALFORMED_UNSPECIFIED
+    assert bool((host(out, np.uint8) == 0x77).all())
+    # (b) an understated extent: the frames past it fail with ZMQG_ERR_BOUND, untouched
+    sizes = [100, 3000, 100, 9000]
+    wire, wire_off, wl, pay_off = _batch(rng, sizes, precom, tamper_every=100)
+    n = len(sizes)
+    dec = C.CurveContext(0, 1)
+    dec.session_set(0, precom, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    total = int(pay_off[-1]) + sizes[-1]
+    out = torch.full((total + 64,), 0x77, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    limit = int(pay_off[2]) + 50  # frame 2 (100 B) and frame 3 reach past it
+    dec.decode_batch(dev(torch, np.zeros(n, np.uint32)), dev(torch, wire_off), dev(torch, wl), dev(torch, wire),
+                     dev(torch, pay_off), out, fl, st, verify_first=True, out_bytes=limit)
+    torch.cuda.synchronize()
+    stt, o = host(st, np.int32), host(out, np.uint8)
+    assert stt[0] == 0 and stt[1] == 0
+    assert stt[2] == C.ERR_BOUND and stt[3] == C.ERR_BOUND
+    assert bool((o[int(pay_off[2]):] == 0x77).all())
