@@ -302,6 +302,26 @@ int main (int argc, char **argv)
     for (int c = 0; c < n_conn; ++c)
         CHECK (a.server[c]->get_peer_nonce () == b.server[c]->get_peer_nonce ());
 
+    {   //  receive slots holding no payload bytes at all (in_used == 0:
+        //  empty frames) and frames under the 33-byte MESSAGE minimum: each
+        //  frame gets its own status through the verify-first decode
+        sink_t esink;
+        zmqg::curve_batcher_t eb (a.ctx, &esink, cfg);
+        CHECK (eb.init () == 0);
+        CHECK (eb.submit_decode (a.server[0], NULL, 0, 1) == 0);
+        CHECK (eb.flush () == 0);
+        CHECK (eb.drain () >= 0);
+        const uint8_t short_frame[20] = {7, 'M', 'E', 'S', 'S', 'A', 'G', 'E'};
+        CHECK (eb.submit_decode (a.server[0], NULL, 0, 2) == 0);
+        CHECK (eb.submit_decode (a.server[1], short_frame, sizeof short_frame, 3) == 0);
+        CHECK (eb.flush () == 0);
+        CHECK (eb.drain () >= 0);
+        CHECK (esink.order.size () == 3);
+        CHECK (esink.got[1].status == ZMQG_ERR_MALFORMED_UNSPECIFIED);
+        CHECK (esink.got[2].status == ZMQG_ERR_MALFORMED_UNSPECIFIED);
+        CHECK (esink.got[3].status == ZMQG_ERR_MALFORMED_MESSAGE);
+    }
+
     free_side (a);
     free_side (b);
     printf ("OK %d\n", n_msgs + n_in);

@@ -13,6 +13,8 @@
 #include <string.h>
 
 #include "salsa_sched_gen.hpp"
+#include "../libzmq_amd/csrc/curve_device.hpp"
+#include "../libzmq_amd/csrc/curve_salsa_asm.hpp"
 
 __device__ unsigned long long g_clk[2];
 
@@ -85,6 +87,42 @@ __global__ __launch_bounds__(256) void k_blk(uint32_t *out, int iters, uint32_t 
     }
 }
 
+// The product's pattern: one key and nonce per lane, the block counter
+// stepping (curve_device.hpp's salsa20_block, where the compiler hoists the
+// counter-free ops, against curve_salsa_asm.hpp's hoisted skewed block).
+template <int V>
+__global__ __launch_bounds__(256) void k_ctr(uint32_t *out, int iters, uint32_t y)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t key[8];
+    for (int i = 0; i < 8; ++i)
+        key[i] = (threadIdx.x + blockIdx.x * 256) * 0x9e3779b9u + i * 0x85ebca6bu + y;
+    const uint32_t n0 = key[3] ^ 0x1234567u, n1 = key[5] + 77u;
+    uint32_t acc[16] = {0};
+    zmqg::SalsaHoist hs;
+    if (V == 1)
+        zmqg::salsa20_hoist(hs, key, n0, n1, 0);
+    for (int it = 0; it < iters; ++it) {
+        uint32_t ks[16];
+        if (V == 0)
+            zmqg::salsa20_block(ks, key, n0, n1, (uint32_t) it, 0);
+        else
+            zmqg::salsa20_block_hoisted(ks, hs, key, n0, n1, (uint32_t) it, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            acc[i] ^= ks[i];
+    }
+    uint32_t *o = out + (size_t) (blockIdx.x * 256 + threadIdx.x) * 32;
+    for (int i = 0; i < 16; ++i) {
+        o[i] = acc[i];
+        o[16 + i] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g_clk[0] = __builtin_amdgcn_s_memtime() - t0;
+        g_clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
+}
+
 typedef void (*KF)(uint32_t *, int, uint32_t);
 int main()
 {
@@ -101,11 +139,12 @@ int main()
     } ks[] = {
         {"compiler x1", k_blk<0, 1>, 1}, {"clump x1", k_blk<1, 1>, 1}, {"skew x1", k_blk<2, 1>, 1},
         {"serial x1", k_blk<3, 1>, 1},   {"compiler x2", k_blk<0, 2>, 2}, {"skew x2", k_blk<2, 2>, 2},
+        {"ctr compiler", k_ctr<0>, 1},   {"ctr hoisted skew", k_ctr<1>, 1},
     };
     // parity: 3 iterations of each order equal the compiler's on the same inputs
     uint32_t *h0 = (uint32_t *) malloc(words * 4), *h1 = (uint32_t *) malloc(words * 4);
     for (auto &k : ks) {
-        KF refk = k.blocks == 1 ? (KF) k_blk<0, 1> : (KF) k_blk<0, 2>;
+        KF refk = k.k == (KF) k_ctr<1> ? (KF) k_ctr<0> : k.blocks == 1 ? (KF) k_blk<0, 1> : (KF) k_blk<0, 2>;
         hipLaunchKernelGGL(refk, dim3(cus), dim3(256), 0, 0, ref, 3, 7u);
         hipLaunchKernelGGL(k.k, dim3(cus), dim3(256), 0, 0, buf, 3, 7u);
         if (hipDeviceSynchronize() != hipSuccess)
