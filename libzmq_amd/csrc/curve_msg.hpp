@@ -43,6 +43,7 @@ struct MsgArgs {
     unsigned long long *peer;      // decode: _cn_peer_nonce per session
     uint8_t *flags_out;            // decode
     int32_t *status;               // decode: 0 / ZMQG_ERR_*; encode: 0 / ZMQG_ERR_SESSION
+    uint32_t *done;                // set to 1 (system scope) after every other write of the launch
     uint64_t nonce;                // encode
     uint32_t sid, len, max_sessions, flags;
 };
@@ -98,6 +99,17 @@ __device__ __forceinline__ fe fe_shfl_down(const fe &x, uint32_t d)
     for (int i = 0; i < 5; ++i)
         y.l[i] = (uint32_t) __shfl_down((int) x.l[i], d, 64);
     return y;
+}
+
+// The launch's completion word: every lane's writes reach memory (system
+// scope: the results sit in mapped host memory), then lane 0 sets it.  The
+// host polls it instead of waiting for the stream (zmqg_*_msg).
+__device__ __forceinline__ void msg_done(uint32_t *done)
+{
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <bool DEC>
@@ -259,6 +271,7 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
             msg_store_g(a.out, st, end, lane);
         if (lane == 0 && a.status)
             *a.status = status;
+        msg_done(a.done);
         return;
     }
     if (status == 0) {
@@ -286,6 +299,7 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
     }
     if (lane == 0)
         *a.status = status;
+    msg_done(a.done);
 }
 
 } // namespace zmqg

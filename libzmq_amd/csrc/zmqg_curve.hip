@@ -37,6 +37,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -2904,7 +2905,26 @@ struct MsgDesc {
     uint64_t nonce, in_off, out_off;
     uint8_t flags, flags_out, pad[2];
     int32_t status;
+    uint32_t done; // k_msg's completion word
 };
+
+// Wait for k_msg's completion word (the kernel's last write, system scope)
+// rather than for the stream: a poll of host memory sees it a few
+// microseconds before a stream synchronisation returns.  Bounded: after
+// 100 ms the stream is synchronised, which also reports a failed launch.
+static int msg_wait(zmqg_ctx *ctx, const MsgDesc *h, hipStream_t st)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE))
+            return 0;
+        if ((spin & 1023u) == 1023u &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100))
+            break;
+    }
+    ZCHECK(ctx, hipStreamSynchronize(st));
+    return __atomic_load_n(&h->done, __ATOMIC_ACQUIRE) ? 0 : -EIO;
+}
 
 // The per-message calls run on the ctx's own stream; work the ctx issued
 // before on another stream (a batch on the caller's stream) shares the
@@ -2936,7 +2956,7 @@ int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, 
     if (rc)
         return rc;
     MsgDesc *h = (MsgDesc *) ctx->mpin;
-    *h = MsgDesc{sid, len, nonce, 0, 0, flags, 0, {0, 0}, 0};
+    *h = MsgDesc{sid, len, nonce, 0, 0, flags, 0, {0, 0}, 0, 0};
     if (len)
         memcpy(ctx->mpin + o_in, in, len);
     uint8_t *d = ctx->mpin_dev;
@@ -2947,11 +2967,12 @@ int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, 
         return rc;
     if (W <= kMsgMaxStream) {
         // one wave, descriptors as arguments (curve_msg.hpp)
-        MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, nullptr, &dd->status, nonce, sid, len,
+        MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, nullptr, &dd->status, &dd->done, nonce, sid, len,
                   ctx->max_sessions, flags};
         hipLaunchKernelGGL(k_msg<false>, dim3(1), dim3(64), 0, st, a);
         ZCHECK(ctx, hipGetLastError());
-        ZCHECK(ctx, hipStreamSynchronize(st));
+        if ((rc = msg_wait(ctx, h, st)))
+            return rc;
         memcpy(out, ctx->mpin + o_out, W);
         return 0;
     }
@@ -2983,7 +3004,7 @@ int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wir
     if (rc)
         return rc;
     MsgDesc *h = (MsgDesc *) ctx->mpin;
-    *h = MsgDesc{sid, wire_len, 0, 0, 0, 0, 0, {0, 0}, 0};
+    *h = MsgDesc{sid, wire_len, 0, 0, 0, 0, 0, {0, 0}, 0, 0};
     if (wire_len)
         memcpy(ctx->mpin + o_in, in, wire_len);
     uint8_t *d = ctx->mpin_dev;
@@ -2993,11 +3014,12 @@ int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wir
     if ((rc = msg_order(ctx)))
         return rc;
     if (wire_len <= kMsgMaxStream) {
-        MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, &dd->flags_out, &dd->status, 0, sid, wire_len,
-                  ctx->max_sessions, 0};
+        MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, &dd->flags_out, &dd->status, &dd->done, 0, sid,
+                  wire_len, ctx->max_sessions, 0};
         hipLaunchKernelGGL(k_msg<true>, dim3(1), dim3(64), 0, st, a);
         ZCHECK(ctx, hipGetLastError());
-        ZCHECK(ctx, hipStreamSynchronize(st));
+        if ((rc = msg_wait(ctx, h, st)))
+            return rc;
         *status_out = h->status;
         *flags_out = h->status == 0 ? h->flags_out : 0;
         if (h->status == 0 && P)
