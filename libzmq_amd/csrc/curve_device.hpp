@@ -74,7 +74,8 @@ __device__ __forceinline__ void salsa20_block(uint32_t out[16], const uint32_t k
 
 // ZMQG_SALSA_SKEW = 1: the hot loops (frame kernels, body kernel) take their
 // keystream blocks from the generated fixed-order core (curve_salsa_asm.hpp,
-// gen_salsa_asm.py); 0: from salsa20_block above.
+// gen_salsa_asm.py); 2: the same, the frame kernels' block in five asm
+// statements; 0: from salsa20_block above.
 #ifndef ZMQG_SALSA_SKEW
 #define ZMQG_SALSA_SKEW 0
 #endif

@@ -450,7 +450,9 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
             for (int k = 0; k < 16; ++k)
                 ks[k] = key[k & 7] ^ (t * 0x9e3779b9u + k);
         } else {
-#if ZMQG_SALSA_SKEW
+#if ZMQG_SALSA_SKEW == 2
+            salsa20_block_hoisted_seg(ks, hs, key, n0, n1, t, 0);
+#elif ZMQG_SALSA_SKEW
             salsa20_block_hoisted(ks, hs, key, n0, n1, t, 0);
 #else
             salsa20_block(ks, key, n0, n1, t, 0);

@@ -134,7 +134,7 @@ def cname(v):
     return "v_" + v.replace(".", "_")
 
 
-def gen_variant(fname_hoist, fname_block, hoist):
+def gen_variant(fname_hoist, fname_block, hoist, segments=1):
     """hoist=True: word 8 (ctr_lo) is the only per-block input; the rest is
     hoisted.  hoist=False: everything per block (no hoist function)."""
     streams, canon, final_ver = build_streams()
@@ -233,18 +233,50 @@ def gen_variant(fname_hoist, fname_block, hoist):
         body.append("    const uint32_t init[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, ctr_lo, ctr_hi,"
                     " SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};")
     body.append("    uint32_t " + ", ".join(f"x{i}" for i in range(16)) + ", t0, t1, t2, t3;")
-    body.append("    asm volatile(")
-    body += [f'        "{t}\\n"' for t in lines_asm]
-    outs = [f'[x{i}] "=&v"(x{i})' for i in range(16)] + [f'[t{j}] "=&v"(t{j})' for j in range(4)]
-    ins = []
-    for i, v in enumerate(need):
-        if v in dyn_inputs:  # a per-block input word (version 0)
-            src = "ctr_lo" if hoist else f"init[{v[1:v.index('.')]}]"
-        else:
-            src = f"hs.v[{hs_index[v]}]"
-        ins.append(f'[h{i}] "v"({src})')
-    body.append("        : " + ",\n          ".join(outs))
-    body.append("        : " + ",\n          ".join(ins) + ");")
+    # the sequence as `segments` asm statements (registers carried across):
+    # code the compiler schedules (e.g. the previous window's Poly1305) can
+    # then sit at the seams instead of before or after the whole block
+    nseg = max(1, segments)
+    bounds = [round(i * len(order) / nseg) for i in range(nseg + 1)]
+    written = set()
+    for sg in range(nseg):
+        chunk = list(range(bounds[sg], bounds[sg + 1]))
+        regs_w, regs_r = [], []
+        for idx in chunk:
+            op = order[idx]
+            for v in (op.s1, op.s2):
+                if v is not None and v in dyn_vals:
+                    r = reg(v)[2:-1]
+                    if r not in regs_r:
+                        regs_r.append(r)
+            r = reg(op.dst)[2:-1]
+            if r not in regs_w:
+                regs_w.append(r)
+        outs = []
+        for r in [f"x{i}" for i in range(16)] + [f"t{j}" for j in range(4)]:
+            if r in written and (r in regs_w or r in regs_r):
+                outs.append(f'[{r}] "+v"({r})')
+            elif r in regs_w:
+                outs.append(f'[{r}] "=&v"({r})')
+        ins = []
+        used_h = set()
+        for idx in chunk:
+            op = order[idx]
+            for v in (op.s1, op.s2):
+                if v is not None and v not in dyn_vals:
+                    used_h.add(need.index(v))
+        for i in sorted(used_h):
+            v = need[i]
+            if v in dyn_inputs:  # a per-block input word (version 0)
+                src = "ctr_lo" if hoist else f"init[{v[1:v.index('.')]}]"
+            else:
+                src = f"hs.v[{hs_index[v]}]"
+            ins.append(f'[h{i}] "v"({src})')
+        body.append("    asm volatile(")
+        body += [f'        "{lines_asm[idx]}\\n"' for idx in chunk]
+        body.append("        : " + ",\n          ".join(outs))
+        body.append("        : " + ",\n          ".join(ins) + ");")
+        written.update(regs_w)
     ff = ["SIGMA0", "k[0]", "k[1]", "k[2]", "k[3]", "SIGMA1", "n0", "n1", "ctr_lo", "ctr_hi", "SIGMA2", "k[4]",
           "k[5]", "k[6]", "k[7]", "SIGMA3"]
     for i in range(16):
@@ -263,6 +295,10 @@ def main():
     parts.append(h)
     b, nb, nv2 = gen_variant(None, "salsa20_block_skew", False)
     parts.append(f"// no hoisting: {nv2} ops per block, every input per block\n" + b)
+    seg = gen_variant(None, "salsa20_block_hoisted_seg", True, segments=5)[0]
+    seg = seg[seg.index("__device__ __forceinline__ void salsa20_block_hoisted_seg"):]
+    parts.append("// the hoisted block as five asm statements (Poly1305 of the previous window\n"
+                 "// can be scheduled at the seams)\n" + seg)
     parts.append("} // namespace zmqg")
     with open(path, "w") as f:
         f.write("\n\n".join(parts) + "\n")
