@@ -47,6 +47,35 @@ def build_batcher_test(out_dir):
     return exe
 
 
+def build_engine_hook_test(out_dir):
+    exe = os.path.join(out_dir, "test_engine_hook")
+    cmd = ["g++", "-O2", "-std=c++11", "-Wall", "-Werror", "-o", exe,
+           os.path.join(ROOT, "tests", "host", "test_engine_hook.cpp"),
+           os.path.join(ROOT, "libzmq_amd", "host", "curve_engine_hook.cpp"),
+           os.path.join(ROOT, "libzmq_amd", "host", "curve_batcher.cpp"),
+           os.path.join(ROOT, "libzmq_amd", "host", "curve_encoding_gpu.cpp"),
+           "-L" + LIB_DIR, "-lzmqg_curve", "-Wl,-rpath," + LIB_DIR,
+           "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib"]
+    subprocess.check_call(cmd)
+    return exe
+
+
+def test_engine_hook_compiles_and_links(tmp_path):
+    assert os.path.exists(build_engine_hook_test(str(tmp_path)))
+
+
+@pytest.mark.gpu
+def test_engine_hook_drives_batcher_like_the_engine(tmp_path):
+    """SURVEY 8f row 1, engine side: curve_io_hook_t / curve_engine_link_t
+    driven by out_event / in_event / poller loops shaped like
+    src/stream_engine_base.cpp:281-291, 331-348 over in-memory sockets, 16
+    connections, a tampered frame failing only its own connection."""
+    exe = build_engine_hook_test(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert r.stdout.strip() == "OK 4800"
+
+
 def test_batcher_compiles_and_links(tmp_path):
     assert os.path.exists(build_batcher_test(str(tmp_path)))
 
