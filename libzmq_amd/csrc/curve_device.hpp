@@ -70,19 +70,6 @@ __device__ __forceinline__ void salsa20_block(uint32_t out[16], const uint32_t k
     out[15] = x[15] + SIGMA3;
 }
 
-} // namespace zmqg
-
-// ZMQG_SALSA_SKEW = 1: the hot loops (frame kernels, body kernel) take their
-// keystream blocks from the generated fixed-order core (curve_salsa_asm.hpp,
-// gen_salsa_asm.py); 2: the same, the frame kernels' block in five asm
-// statements; 0: from salsa20_block above.
-#ifndef ZMQG_SALSA_SKEW
-#define ZMQG_SALSA_SKEW 0
-#endif
-#include "curve_salsa_asm.hpp"
-
-namespace zmqg {
-
 // HSalsa20(k, in[4 words]) -> 8-word subkey (no feed-forward).
 __device__ __forceinline__ void hsalsa20(uint32_t out[8], const uint32_t k[8], const uint32_t in[4])
 {

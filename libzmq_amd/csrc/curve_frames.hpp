@@ -1269,10 +1269,6 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
     uint32_t cp[16];  // ciphertext of the window whose MAC is absorbed next step
     uint32_t cp_j0 = 2, cp_len = 0; // its first block slot and ciphertext bytes
     uint32_t ycarry;  // last output word of the previous window
-#if ZMQG_SALSA_SKEW
-    SalsaHoist hs; // the counter-free part of every block of this lane's frame
-    salsa20_hoist(hs, key, n0, n1, 0);
-#endif
     {
         uint32_t ks[16];
         salsa20_block(ks, key, n0, n1, 0, 0);
@@ -1372,13 +1368,7 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
             for (int k = 0; k < 16; ++k)
                 ks[k] = key[k & 7] ^ (t * 0x9e3779b9u + k);
         } else {
-#if ZMQG_SALSA_SKEW == 2
-            salsa20_block_hoisted_seg(ks, hs, key, n0, n1, t, 0);
-#elif ZMQG_SALSA_SKEW
-            salsa20_block_hoisted(ks, hs, key, n0, n1, t, 0);
-#else
             salsa20_block(ks, key, n0, n1, t, 0);
-#endif
         }
         // The previous window's MAC (its ciphertext is in cp).  The
         // four-block form runs for every lane, unconditionally, so that it

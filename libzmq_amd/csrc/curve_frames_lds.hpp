@@ -355,10 +355,6 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     uint32_t spad[4], wtag[4] = {0, 0, 0, 0}, fl = 0;
     uint32_t cp[16];                // ciphertext of the window whose MAC is absorbed next step
     uint32_t cp_j0 = 2, cp_len = 0; // its first block slot and ciphertext bytes
-#if ZMQG_SALSA_SKEW
-    SalsaHoist hs; // the counter-free part of every block of this lane's frame
-    salsa20_hoist(hs, key, n0, n1, 0);
-#endif
     {
         uint32_t ks[16];
         salsa20_block(ks, key, n0, n1, 0, 0);
@@ -450,13 +446,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
             for (int k = 0; k < 16; ++k)
                 ks[k] = key[k & 7] ^ (t * 0x9e3779b9u + k);
         } else {
-#if ZMQG_SALSA_SKEW == 2
-            salsa20_block_hoisted_seg(ks, hs, key, n0, n1, t, 0);
-#elif ZMQG_SALSA_SKEW
-            salsa20_block_hoisted(ks, hs, key, n0, n1, t, 0);
-#else
             salsa20_block(ks, key, n0, n1, t, 0);
-#endif
         }
         // The previous window's MAC (its ciphertext is in cp), the four-block
         // form for every lane, unconditionally, in the keystream's basic block

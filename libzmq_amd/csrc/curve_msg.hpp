@@ -92,6 +92,32 @@ __device__ __forceinline__ void msg_zero_g(uint8_t *g, uint32_t n, uint32_t lane
         g[k] = 0;
 }
 
+// Carry a sum of two partially reduced elements (limbs below 2^28) back to
+// limbs below 2^26 (limb 1 below 2^26 + 1): fe_mul's inputs must stay below
+// 2^27, or its last fold (c * 5 in 32 bits) wraps.
+__device__ __forceinline__ void fe_carry(fe &h)
+{
+    uint32_t c;
+    c = h.l[0] >> 26;
+    h.l[0] &= M26;
+    h.l[1] += c;
+    c = h.l[1] >> 26;
+    h.l[1] &= M26;
+    h.l[2] += c;
+    c = h.l[2] >> 26;
+    h.l[2] &= M26;
+    h.l[3] += c;
+    c = h.l[3] >> 26;
+    h.l[3] &= M26;
+    h.l[4] += c;
+    c = h.l[4] >> 26;
+    h.l[4] &= M26;
+    h.l[0] += c * 5;
+    c = h.l[0] >> 26;
+    h.l[0] &= M26;
+    h.l[1] += c;
+}
+
 __device__ __forceinline__ fe fe_shfl_down(const fe &x, uint32_t d)
 {
     fe y;
@@ -248,6 +274,7 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
         if ((lane & ((2u << s) - 1u)) == 0) {
             fe_mul(h, p);
             fe_add(h, hn);
+            fe_carry(h); // (the next level multiplies it again)
         }
         if (s < 5)
             fe_mul(p, p);

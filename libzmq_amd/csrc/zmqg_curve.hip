@@ -1702,11 +1702,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
             for (int q = 0; q < 16; ++q)
                 ks[q] = tw * 16 + q;
 #else
-#if ZMQG_SALSA_SKEW
-            salsa20_block_skew(ks, cur.k, cur.n0, cur.n1, 1 + 2 * cur.c + tw, 0);
-#else
             salsa20_block(ks, cur.k, cur.n0, cur.n1, 1 + 2 * cur.c + tw, 0);
-#endif
 #endif
             if (DEC && ZMQG_ABLATE != 2) {
                 if (__all(nv == 64))

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Generates curve_salsa_asm.hpp: the Salsa20/20 core with a fixed issue
-order for gfx950, as inline assembly.
+order for gfx950, as inline assembly (round-4 experiment, measured by
+tools/salsa_sched.hip and in the library's frame and body kernels: no gain
+at any occupancy -- every order issues at ~4 cycles per instruction,
+DESIGN.md section 3.1; not in the product).
 
 Why a fixed order.  A Salsa20 step b ^= rotl(a + d, k) is v_add_u32 (VOP2),
 v_alignbit_b32 (the rotate, VOP3) and v_xor_b32 (VOP2).  Once two waves

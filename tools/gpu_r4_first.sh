@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 timeout -k 10 120 ./build/salsa_sched > gpurun_out/salsa_sched.json 2>&1 || { cat gpurun_out/salsa_sched.json; exit 1; }
 cat gpurun_out/salsa_sched.json
-timeout -k 10 600 python -u -m pytest tests/test_gpu_msg.py tests/test_gpu_session_batch.py tests/test_host_adapter.py tests/test_gpu_verify_first.py tests/test_gpu_bench_batches.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_new.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_msg.py tests/test_gpu_session_batch.py tests/test_host_adapter.py tests/test_gpu_multirank.py tests/test_gpu_verify_first.py tests/test_gpu_bench_batches.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_new.log 2>&1
 echo "pytest_new rc=$?"; tail -30 gpurun_out/pytest_new.log
 timeout -k 10 120 ./build/msg_latency > gpurun_out/msg_latency.json 2>&1; echo "msg_latency rc=$?"; cat gpurun_out/msg_latency.json
 for v in 1 2; do

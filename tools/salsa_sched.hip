@@ -6,6 +6,7 @@
 // (profiles/valu_rates_r02.md: an independent 2 VOP2 : 1 VOP3 mix issues at
 // ~2.9 cycles per instruction at two waves, the compiler's Salsa20 block at ~4).
 // Build: python3 tools/gen_salsa_sched.py build/salsa_sched_gen.hpp &&
+//        python3 tools/gen_salsa_asm.py build/curve_salsa_asm.hpp &&
 //        hipcc -O3 --offload-arch=gfx950 -Ibuild -o build/salsa_sched tools/salsa_sched.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -14,7 +15,7 @@
 
 #include "salsa_sched_gen.hpp"
 #include "../libzmq_amd/csrc/curve_device.hpp"
-#include "../libzmq_amd/csrc/curve_salsa_asm.hpp"
+#include "curve_salsa_asm.hpp" // tools/gen_salsa_asm.py
 
 __device__ unsigned long long g_clk[2];
 
