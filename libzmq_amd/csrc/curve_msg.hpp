@@ -48,10 +48,30 @@ struct MsgArgs {
     uint32_t sid, len, max_sessions, flags;
 };
 
-// byte-granular copies between global memory and LDS: 4-byte words where
-// both sides allow it, bytes at the edges
+// Copies between global memory and LDS.  The message sits in mapped host
+// memory, so a load is a PCIe round trip: a 16-byte-aligned message (the
+// per-message buffer always is) is read with all of a lane's loads in
+// flight at once -- up to four dwordx4 per lane, 4 KiB per wave -- before any
+// of them is used; other alignments take the general byte/word form.
+typedef u32x4 msg_u32x4_u1 __attribute__((aligned(1)));
 __device__ __forceinline__ void msg_load_lds(uint8_t *lds, const uint8_t *g, uint32_t n, uint32_t lane)
 {
+    if (((uintptr_t) g & 15u) == 0 && n <= kMsgMaxStream) {
+        const uint32_t ng = n >> 4, tail = n & 15u;
+        u32x4 v[kMsgMaxStream / 16 / 64];
+#pragma unroll
+        for (uint32_t j = 0; j < kMsgMaxStream / 16 / 64; ++j)
+            if (lane + 64u * j < ng)
+                v[j] = *(const GCU4 *) (uintptr_t) (g + 16u * (lane + 64u * j));
+        const uint8_t tb = lane < tail ? g[16u * ng + lane] : 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kMsgMaxStream / 16 / 64; ++j)
+            if (lane + 64u * j < ng)
+                *(msg_u32x4_u1 *) (lds + 16u * (lane + 64u * j)) = v[j];
+        if (lane < tail)
+            lds[16u * ng + lane] = tb;
+        return;
+    }
     const uint32_t head = (4u - ((uint32_t) (uintptr_t) g & 3u)) & 3u;
     const uint32_t h = head < n ? head : n;
     for (uint32_t k = lane; k < h; k += 64)
@@ -130,16 +150,81 @@ __device__ __forceinline__ fe fe_shfl_down(const fe &x, uint32_t d)
 // The launch's completion word: every lane's writes reach memory (system
 // scope: the results sit in mapped host memory), then lane 0 sets it.  The
 // host polls it instead of waiting for the stream (zmqg_*_msg).
+#ifndef ZMQG_MSG_ABLATE
+#define ZMQG_MSG_ABLATE 0 // (diagnostic builds only: 1 release-only fence, 2 no fence, 4 no Salsa20,
+                          // 8 no Poly1305 tree, 16 no output stores, 32 no input loads)
+#endif
 __device__ __forceinline__ void msg_done(uint32_t *done)
 {
+    if (ZMQG_MSG_ABLATE & 2) {
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (ZMQG_MSG_ABLATE & 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <bool DEC>
-__global__ __launch_bounds__(64) void k_msg(MsgArgs a)
+// salsa20_block with the double rounds in a loop: a single launch executes
+// it once per lane, so a tenth of the code (fewer instruction-cache misses
+// on a cold CU) costs only the loop's scalar branch.
+__device__ __forceinline__ void salsa20_block_rolled(uint32_t out[16], const uint32_t k[8], uint32_t n0, uint32_t n1,
+                                                     uint32_t ctr)
+{
+    uint32_t x[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, ctr, 0, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+#pragma unroll 1
+    for (int rr = 0; rr < 10; ++rr) {
+        ZMQG_QR(x[0], x[4], x[8], x[12]);
+        ZMQG_QR(x[5], x[9], x[13], x[1]);
+        ZMQG_QR(x[10], x[14], x[2], x[6]);
+        ZMQG_QR(x[15], x[3], x[7], x[11]);
+        ZMQG_QR(x[0], x[1], x[2], x[3]);
+        ZMQG_QR(x[5], x[6], x[7], x[4]);
+        ZMQG_QR(x[10], x[11], x[8], x[9]);
+        ZMQG_QR(x[15], x[12], x[13], x[14]);
+    }
+    const uint32_t in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, ctr, 0, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        out[i] = x[i] + in[i];
+}
+
+// The message itself as a kernel argument (CAP bytes, zero-padded to a
+// whole word): kernel arguments reach the GPU with the dispatch, so the
+// kernel reads them at HBM latency instead of pulling the message over PCIe
+// from mapped host memory (a 4,000-byte message cost ~5 us of PCIe reads).
+template <uint32_t CAP>
+struct MsgInline {
+    uint32_t w[CAP ? CAP / 4 : 1];
+};
+constexpr uint32_t kMsgInlineMax = 3968; // kernel arguments are limited to 4 KiB in all
+
+// LDS <- the inline message (n bytes) at byte offset lds (any alignment)
+typedef uint32_t msg_u32_u1 __attribute__((aligned(1)));
+template <uint32_t CAP>
+__device__ __forceinline__ void msg_inline_lds(uint8_t *lds, const MsgInline<CAP> &d, uint32_t n, uint32_t lane)
+{
+    const uint32_t nw = (n + 3) >> 2;
+#pragma unroll
+    for (uint32_t j = 0; j < (CAP / 4 + 63) / 64; ++j) {
+        const uint32_t i = lane + 64u * j;
+        if (i < nw)
+            *(msg_u32_u1 *) (lds + 4u * i) = d.w[i];
+    }
+}
+
+template <bool DEC, uint32_t CAP>
+__global__ __launch_bounds__(64) void k_msg(MsgArgs a, MsgInline<CAP> d)
 {
     __shared__ uint32_t st_w[kMsgMaxStream / 4 + 16]; // the stream image: 32 bytes, then the message bytes
     uint8_t *const st = (uint8_t *) st_w;
@@ -150,6 +235,9 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
 #pragma unroll
     for (int t = 0; t < 8; ++t)
         key[t] = DEC ? ses.dec_key[t] : ses.enc_key[t];
+    // decode: the peer nonce is read now, beside the message's PCIe round
+    // trip, not after it
+    const unsigned long long peer = DEC && sid_ok ? a.peer[a.sid] : 0ull;
 
     // ---- 1. the message into LDS at its stream position; header checks
     uint32_t m = 0; // ciphertext bytes
@@ -164,7 +252,10 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
             st_w[lane] = 0;
         if (lane < hl)
             st[32 + lane] = (uint8_t) (hw[lane >> 2] >> (8 * (lane & 3)));
-        msg_load_lds(st + 32 + hl, a.in, a.len, lane);
+        if (CAP)
+            msg_inline_lds(st + 32 + hl, d, a.len, lane);
+        else if (!(ZMQG_MSG_ABLATE & 32))
+            msg_load_lds(st + 32 + hl, a.in, a.len, lane);
         nc = a.nonce;
         n0 = bswap32((uint32_t) (nc >> 32));
         n1 = bswap32((uint32_t) nc);
@@ -172,7 +263,10 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
             status = ZMQG_ERR_SESSION;
     } else {
         const uint32_t L = a.len;
-        msg_load_lds(st, a.in, L, lane);
+        if (CAP)
+            msg_inline_lds(st, d, L, lane);
+        else if (!(ZMQG_MSG_ABLATE & 32))
+            msg_load_lds(st, a.in, L, lane);
         __syncthreads();
         // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
         const uint32_t b0 = L ? st[0] : 0u;
@@ -192,7 +286,6 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
             nc = ((uint64_t) bswap32(n0) << 32) | bswap32(n1);
             // curve_mechanism_base.cpp:98-106: a nonce not above the peer's
             // is a replay; a valid one becomes the peer nonce before the MAC
-            const unsigned long long peer = a.peer[a.sid];
             if (nc <= peer)
                 status = ZMQG_ERR_INVALID_SEQUENCE;
         }
@@ -209,7 +302,13 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
     // ---- 2. keystream block `lane`, XOR of its window
     const uint32_t nb = (end + 63) >> 6;
     uint32_t ks[16];
-    salsa20_block(ks, key, n0, n1, lane, 0);
+    if (ZMQG_MSG_ABLATE & 4) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            ks[k] = key[k & 7] ^ (lane * 0x9e3779b9u + k);
+    } else {
+        salsa20_block_rolled(ks, key, n0, n1, lane);
+    }
     uint32_t w[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -240,10 +339,16 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
 
     // ---- 3. Poly1305 over the ciphertext (stream bytes 32 .. 32+m)
     const fe r = poly_r_from_key(pk[0], pk[1], pk[2], pk[3]);
+    // nl lanes of four blocks each, right-aligned in the smallest power-of-
+    // two span S that holds them (a short message needs few or no levels)
     const uint32_t N = (m + 15) >> 4, nl = (N + 3) >> 2, pad = 4 * nl - N;
+    uint32_t levels = 0;
+    while ((1u << levels) < nl)
+        ++levels;
+    const uint32_t S = 1u << levels;
     fe h = fe_zero();
-    const int seg = (int) lane - (int) (64 - nl);
-    if (seg >= 0) {
+    const int seg = (int) lane - (int) (S - nl);
+    if (seg >= 0 && lane < S) {
         const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -265,19 +370,22 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
             }
         }
     }
-    fe p = r;
-    fe_mul(p, r);
-    fe_mul(p, p); // r^4
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-        const fe hn = fe_shfl_down(h, 1u << s);
-        if ((lane & ((2u << s) - 1u)) == 0) {
-            fe_mul(h, p);
-            fe_add(h, hn);
-            fe_carry(h); // (the next level multiplies it again)
+    if (levels && !(ZMQG_MSG_ABLATE & 8)) {
+        fe p = r;
+        fe_mul(p, r);
+        fe_mul(p, p); // r^4
+        // (a rolled loop: one launch runs this once, from a cold instruction cache)
+#pragma unroll 1
+        for (uint32_t s = 0; s < levels; ++s) {
+            const fe hn = fe_shfl_down(h, 1u << s);
+            if ((lane & ((2u << s) - 1u)) == 0) {
+                fe_mul(h, p);
+                fe_add(h, hn);
+                fe_carry(h); // (the next level multiplies it again)
+            }
+            if (s + 1 < levels)
+                fe_mul(p, p);
         }
-        if (s < 5)
-            fe_mul(p, p);
     }
     uint32_t tag[4];
     poly_finish(h, pk + 4, tag);
@@ -295,7 +403,8 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
         }
         __syncthreads();
         if (status == 0)
-            msg_store_g(a.out, st, end, lane);
+            if (!(ZMQG_MSG_ABLATE & 16))
+                msg_store_g(a.out, st, end, lane);
         if (lane == 0 && a.status)
             *a.status = status;
         msg_done(a.done);
@@ -316,11 +425,13 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a)
             for (int k = 0; k < 16; ++k)
                 st_w[16 * lane + k] = o[k];
         __syncthreads();
-        msg_store_g(a.out, st + 33, P, lane);
+        if (!(ZMQG_MSG_ABLATE & 16))
+            msg_store_g(a.out, st + 33, P, lane);
         if (lane == 0)
             *a.flags_out = st[32] & 3u; // msg_t::more | msg_t::command (curve_mechanism_base.cpp:276)
     } else {
-        msg_zero_g(a.out, P, lane);
+        if (!(ZMQG_MSG_ABLATE & 16))
+            msg_zero_g(a.out, P, lane);
         if (lane == 0)
             *a.flags_out = 0;
     }

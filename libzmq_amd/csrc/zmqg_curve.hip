@@ -2234,6 +2234,28 @@ int replay_multi(zmqg_ctx *ctx, uint32_t nn, const uint32_t *sid, hipStream_t st
 
 } // namespace
 
+// k_msg with the message inline in its arguments when it fits one of the
+// tiers (the argument block is copied whole, so small messages take a small
+// tier), else read from the mapped buffer.
+template <bool DEC>
+static void launch_msg(hipStream_t st, const MsgArgs &a, const uint8_t *msg, uint32_t n)
+{
+    auto go = [&](auto inl) {
+        memset(inl.w, 0, sizeof inl.w);
+        if (n)
+            memcpy(inl.w, msg, n);
+        hipLaunchKernelGGL((k_msg<DEC, sizeof inl.w>), dim3(1), dim3(64), 0, st, a, inl);
+    };
+    if (n <= 256u)
+        go(MsgInline<256>{});
+    else if (n <= 1024)
+        go(MsgInline<1024>{});
+    else if (n <= kMsgInlineMax)
+        go(MsgInline<kMsgInlineMax>{});
+    else
+        hipLaunchKernelGGL((k_msg<DEC, 0>), dim3(1), dim3(64), 0, st, a, MsgInline<0>{});
+}
+
 extern "C" {
 
 int zmqg_abi_version(void)
@@ -2953,7 +2975,7 @@ int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, 
         return rc;
     MsgDesc *h = (MsgDesc *) ctx->mpin;
     *h = MsgDesc{sid, len, nonce, 0, 0, flags, 0, {0, 0}, 0, 0};
-    if (len)
+    if (len && (W > kMsgMaxStream || len > kMsgInlineMax)) // (else the message travels as a kernel argument)
         memcpy(ctx->mpin + o_in, in, len);
     uint8_t *d = ctx->mpin_dev;
     MsgDesc *dd = (MsgDesc *) d;
@@ -2965,7 +2987,7 @@ int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, 
         // one wave, descriptors as arguments (curve_msg.hpp)
         MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, nullptr, &dd->status, &dd->done, nonce, sid, len,
                   ctx->max_sessions, flags};
-        hipLaunchKernelGGL(k_msg<false>, dim3(1), dim3(64), 0, st, a);
+        launch_msg<false>(st, a, in, len);
         ZCHECK(ctx, hipGetLastError());
         if ((rc = msg_wait(ctx, h, st)))
             return rc;
@@ -3001,7 +3023,7 @@ int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wir
         return rc;
     MsgDesc *h = (MsgDesc *) ctx->mpin;
     *h = MsgDesc{sid, wire_len, 0, 0, 0, 0, 0, {0, 0}, 0, 0};
-    if (wire_len)
+    if (wire_len && (wire_len > kMsgMaxStream || wire_len > kMsgInlineMax))
         memcpy(ctx->mpin + o_in, in, wire_len);
     uint8_t *d = ctx->mpin_dev;
     MsgDesc *dd = (MsgDesc *) d;
@@ -3012,7 +3034,7 @@ int zmqg_decode_msg(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint32_t wir
     if (wire_len <= kMsgMaxStream) {
         MsgArgs a{d + o_in, d + o_out, ctx->sessions, ctx->peer, &dd->flags_out, &dd->status, &dd->done, 0, sid,
                   wire_len, ctx->max_sessions, 0};
-        hipLaunchKernelGGL(k_msg<true>, dim3(1), dim3(64), 0, st, a);
+        launch_msg<true>(st, a, in, wire_len);
         ZCHECK(ctx, hipGetLastError());
         if ((rc = msg_wait(ctx, h, st)))
             return rc;

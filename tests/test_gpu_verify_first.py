@@ -134,10 +134,14 @@ def test_verify_first_extent_checks(torch_cuda, C):
     torch = torch_cuda
     rng = np.random.default_rng(91)
     precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
-    # (a) no payload bytes at all: out_bytes = 0
-    sizes = [0, 0, 0]
-    wire, wire_off, wl, _ = _batch(rng, sizes, precom, tamper_every=100)
-    wl = wl.copy()
+    # (a) no payload bytes at all: out_bytes = 0 -- a valid empty message, a
+    # frame cut below the MESSAGE minimum, an empty frame
+    n = 3
+    wl = np.full(n, 33, np.uint32)
+    wire_off = np.arange(n, dtype=np.uint64) * 33
+    wire = O.encode_batch(O.make_sessions([precom]), np.zeros(n, np.uint32), np.arange(3, 3 + n, dtype=np.uint64),
+                          np.zeros(n, np.uint8), np.zeros(n, np.uint64), np.zeros(n, np.uint32),
+                          np.zeros(1, np.uint8), wire_off, 33 * n)
     wl[1] = 20  # shorter than a MESSAGE
     wl[2] = 0   # empty
     dec = C.CurveContext(0, 1)
@@ -154,6 +158,9 @@ def test_verify_first_extent_checks(torch_cuda, C):
     # (b) an understated extent: the frames past it fail with ZMQG_ERR_BOUND, untouched
     sizes = [100, 3000, 100, 9000]
     wire, wire_off, wl, pay_off = _batch(rng, sizes, precom, tamper_every=100)
+    wire = wire.copy()  # (_batch tampers frame 0's ciphertext and frame 2's name: undo both)
+    wire[wire_off[0] + 32 + sizes[0] // 2] ^= 0x40
+    wire[wire_off[2] + 1] ^= 0x20
     n = len(sizes)
     dec = C.CurveContext(0, 1)
     dec.session_set(0, precom, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)

@@ -1,7 +1,8 @@
 """The parallel Poly1305 of the one-message kernel (libzmq_amd/csrc/
 curve_msg.hpp, k_msg): a CPU model of its limb arithmetic -- per-lane Horner
-over four 16-byte blocks with the lanes placed at the end of the wave, six
-shuffle levels h_v = h_v * r^(4*2^s) + h_(v+2^s), the 26-bit-limb multiply of
+over four 16-byte blocks with the lanes placed at the end of the smallest
+power-of-two span of lanes that holds them, log2(span) shuffle levels
+h_v = h_v * r^(4*2^s) + h_(v+2^s), the 26-bit-limb multiply of
 curve_device.hpp's fe_mul_s with its 32-bit intermediates -- against plain
 Poly1305 (RFC 8439 / libsodium 1.0.18) on random keys and block counts.
 
@@ -74,11 +75,15 @@ def tree_poly(blocks, r, carry=True):
     rf = to_fe(r)
     nl = (n + 3) // 4
     pad = 4 * nl - n
+    levels = 0
+    while (1 << levels) < nl:
+        levels += 1
+    span = 1 << levels  # the lanes right-aligned in the smallest power-of-two span
     hs = []
     for lane in range(64):
-        seg = lane - (64 - nl)
+        seg = lane - (span - nl)
         h = [0] * 5
-        if seg >= 0:
+        if seg >= 0 and lane < span:
             for t in range(4):
                 k = 4 * seg + t - pad
                 if k >= 0:
@@ -87,12 +92,12 @@ def tree_poly(blocks, r, carry=True):
                     h = fe_mul([h[i] + m[i] for i in range(5)], rf)
         hs.append(h)
     p = fe_mul(fe_mul(rf, rf), fe_mul(rf, rf))
-    for s in range(6):
+    for s in range(levels):
         for v in range(0, 64, 2 << s):
             h = fe_mul(hs[v], p)
             h = [h[i] + hs[v + (1 << s)][i] for i in range(5)]
             hs[v] = fe_carry(h) if carry else h
-        if s < 5:
+        if s + 1 < levels:
             p = fe_mul(p, p)
     return from_fe(hs[0]) % P
 
