@@ -353,7 +353,19 @@ struct FrameCtl {
     unsigned long long *nonce_ctr; // encode, one session, ZMQG_OPT_NONCE_AUTO: the session's send
                                    // counter; frame i takes *nonce_ctr + i, the last workgroup adds n
     uint64_t out_limit;  // (out_check) the caller's out_bytes: the staging area's extent
+    const uint8_t *zflags; // decode from zmqg_decode_zmtp: each frame's ZMTP flags byte (or null)
 };
+
+// msg_t flags a received ZMTP frame adds to its decoded message: the
+// decoder's MORE / COMMAND (src/v2_decoder.cpp:35-41) ORed into the
+// plaintext's by set_flags (src/msg.cpp:433-436); 0 without zflags.
+__device__ __forceinline__ uint32_t zmtp_msg_bits(const uint8_t *zflags, uint32_t i)
+{
+    if (!zflags)
+        return 0u;
+    const uint32_t z = zflags[i];
+    return (z & 1u) | ((z & 4u) ? 2u : 0u); // ZMTP MORE (1) / COMMAND (4) -> msg_t more (1) / command (2)
+}
 
 // A frame the call must not process (status ZMQG_ERR_BOUND, nothing
 // written): above the caller's max_len, or -- decode under
@@ -989,7 +1001,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
         else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
         status_out[i] = status;
-        flags_out[i] = status == 0 ? (uint8_t) fl : 0;
+        flags_out[i] = status == 0 ? (uint8_t) (fl | zmtp_msg_bits(ctl.zflags, i)) : 0;
         if (status != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the group's plaintext stores first
             zero_bytes(dst, S - 33u);
@@ -1591,7 +1603,7 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
         else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
         status_out[i] = status;
-        flags_out[i] = status == 0 ? (uint8_t) fl : 0;
+        flags_out[i] = status == 0 ? (uint8_t) (fl | zmtp_msg_bits(ctl.zflags, i)) : 0;
         if (status != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this lane's plaintext stores first
             zero_bytes(dst, S - 33u);

@@ -563,7 +563,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
         status_out[i] = status;
-        flags_out[i] = status == 0 ? (uint8_t) fl : 0;
+        flags_out[i] = status == 0 ? (uint8_t) (fl | zmtp_msg_bits(ctl.zflags, i)) : 0;
         if (status != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the wave's stores of this frame first
             zero_bytes(dst, S - 33u);

@@ -179,6 +179,9 @@ struct ZmtpWs {
     uint8_t *fflags = nullptr;            // [f_cap]
     ZmtpWalk *walk = nullptr;
     zmqg_zmtp_result *res = nullptr;      // the synchronous call's result on the device
+    ZmtpBar *bar = nullptr;               // k_zmtp_chain's grid barrier (zeroed once)
+    unsigned long long *part = nullptr;   // [chain_grid] k_zmtp_chain's per-workgroup count shares
+    uint32_t chain_grid = 0;              // k_zmtp_chain's workgroups (0: not yet sized; ~0u: no cooperative launch)
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };
@@ -1597,7 +1600,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
     const FrameHot *__restrict__ hot, const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
     const uint32_t *__restrict__ powtab, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
     unsigned long long *__restrict__ acc, uint32_t *__restrict__ cnt, const unsigned long long *__restrict__ excl,
-    const unsigned long long *__restrict__ psnap, PostOp *__restrict__ post)
+    const unsigned long long *__restrict__ psnap, PostOp *__restrict__ post, const uint8_t *__restrict__ zflags)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kBodyWaves * 2 * kBufLds];
     const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1900,7 +1903,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
                                            : diff              ? ZMQG_ERR_CRYPTOGRAPHIC // :277-281
                                                                : 0;
                     status_out[i] = status;
-                    flags_out[i] = status == 0 ? (uint8_t) (cur.flags & 3u) : 0;
+                    flags_out[i] = status == 0 ? (uint8_t) ((cur.flags & 3u) | zmtp_msg_bits(zflags, i)) : 0;
                     // k_post, after every tile of this call: a failed frame's
                     // region is zero-filled (its tiles' plaintext may still sit
                     // dirty in other XCDs' L2s, so not here), an in-place frame
@@ -2672,7 +2675,7 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         hipLaunchKernelGGL(k_body<false>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
                            w.pw, w.fin, w.powtab, (uint8_t *) nullptr, (int32_t *) nullptr, w.acc, w.cnt,
                            (const unsigned long long *) nullptr, (const unsigned long long *) nullptr,
-                           (PostOp *) nullptr);
+                           (PostOp *) nullptr, (const uint8_t *) nullptr);
         ZCHECK(ctx, hipGetLastError());
         body.end();
     }
@@ -2687,9 +2690,12 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
     return zmqg_encode_batch_ex(ctx, n, sid, nonce, flags, in_off, len, in, out_off, out, nullptr, stream);
 }
 
-int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
-                         const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
-                         uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts, void *stream)
+// zmqg_decode_batch_ex; zflags (zmqg_decode_zmtp): each frame's ZMTP flags
+// byte, whose MORE / COMMAND bits the decode ORs into flags_out
+static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                             const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
+                             uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts,
+                             const uint8_t *zflags, void *stream)
 {
     if (!ctx || check_n(n) || check_opts(opts))
         return -EINVAL;
@@ -2727,6 +2733,7 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     const bool multi = ctx->sort_bits > 0;
     FrameCtl ctl{};
     ctl.post = w.post;
+    ctl.zflags = zflags;
     unsigned long long *smax = nullptr;
     if (opts) {
         ctl.max_len = opts->max_len;
@@ -2772,7 +2779,7 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     if (!ctl.no_body) {
         ProfSpan body(ctx, ZMQG_PROF_DECODE_BODY, st);
         hipLaunchKernelGGL(k_body<true>, dim3(body_grid(ctx)), dim3(kBodyThreads), 0, st, w.zs, w.chunk_end, w.hot,
-                           w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap, w.post);
+                           w.pw, w.fin, w.powtab, flags_out, status_out, w.acc, w.cnt, w.excl, w.psnap, w.post, zflags);
         ZCHECK(ctx, hipGetLastError());
         hipLaunchKernelGGL(k_post, dim3(body_grid(ctx)), dim3(256), 0, st, w.zs, (const PostOp *) w.post,
                            (uint8_t *) w.powtab);
@@ -2793,6 +2800,14 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     }
     call.end();
     return 0;
+}
+
+int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
+                         const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
+                         uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts, void *stream)
+{
+    return decode_batch_impl(ctx, n, sid, in_off, wire_len, in, out_off, out, flags_out, status_out, opts, nullptr,
+                             stream);
 }
 
 int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
@@ -3160,6 +3175,14 @@ int zmqg_encode_zmtp(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     return zmqg_encode_batch(ctx, n, sid, nonce, flags, in_off, len, in, z.wire_off, out, stream);
 }
 
+// the candidate scan: the shuffle form unless ZMQG_ZMTP_SCAN1 is set (the
+// three-load form, kept for A/B runs)
+static void (*zmtp_scan_kernel())(const uint8_t *, uint64_t, int64_t, uint64_t *, uint64_t *)
+{
+    static const bool one = getenv("ZMQG_ZMTP_SCAN1") != nullptr;
+    return one ? k_zmtp_scan<false> : k_zmtp_scan<true>;
+}
+
 int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
                            uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
                            uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result,
@@ -3211,13 +3234,88 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
     if (!z.walk && (rc = grow(ctx, z.walk, 1, st)))
         return rc;
     const uint32_t g = (uint32_t) nwg;
+    // The middle in one launch (k_zmtp_chain, one workgroup per CU, grid
+    // barriers) unless the device cannot hold that grid at once or
+    // ZMQG_ZMTP_SPLIT is set (the separate launches below, kept for A/B runs).
+    if (!z.chain_grid) {
+        int nb = 0;
+        ZCHECK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_zmtp_chain, kZmtpThreads, 0));
+        const int cus = ctx->cus > 0 ? ctx->cus : 1;
+        z.chain_grid = nb > 0 && getenv("ZMQG_ZMTP_SPLIT") == nullptr ? (uint32_t) cus : ~0u;
+        if (z.chain_grid != ~0u) {
+            if ((rc = grow(ctx, z.bar, 1, st)) || (rc = grow(ctx, z.part, z.chain_grid, st)))
+                return rc;
+            ZCHECK(ctx, hipMemsetAsync(z.bar, 0, sizeof(ZmtpBar), st));
+        }
+    }
+    const bool chain = z.chain_grid != ~0u;
+    if (chain) {
+        hipLaunchKernelGGL(zmtp_scan_kernel(), dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
+                           z.count_wg);
+        ZCHECK(ctx, hipGetLastError());
+        ZmtpChainArgs a{};
+        a.b = in;
+        a.n = in_bytes;
+        a.max_msg = max_msg_size;
+        a.max_frames = max_frames;
+        a.cand_wg = z.cand_wg;
+        a.count_wg = z.count_wg;
+        a.nwg = nwg;
+        a.off_wg = z.off_wg;
+        a.part = z.part;
+        a.cand = z.cand;
+        a.nb = z.nb;
+        a.first_seg = z.first_seg;
+        a.run = z.run;
+        a.runpre = z.runpre;
+        a.walk = z.walk;
+        a.f_off = frame_in_off;
+        a.f_len = frame_len;
+        a.f_flags = z.fflags;
+        a.sid_fill = z.sid_fill;
+        a.sid = sid;
+        a.out_off = out_off;
+        a.bar = z.bar;
+        a.res = result;
+        static const bool clk = getenv("ZMQG_ZMTP_CLK") != nullptr; // diagnostics: phase times to stderr
+        if (clk)
+            ZCHECK(ctx, hipMallocAsync((void **) &a.clk, 8ull * z.chain_grid * sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(k_zmtp_chain, dim3(z.chain_grid), dim3(kZmtpThreads), 0, st, a);
+        ZCHECK(ctx, hipGetLastError());
+        if (clk) {
+            std::vector<unsigned long long> h(8ull * z.chain_grid);
+            ZCHECK(ctx, hipMemcpyAsync(h.data(), a.clk, h.size() * 8, hipMemcpyDeviceToHost, st));
+            ZCHECK(ctx, hipStreamSynchronize(st));
+            ZCHECK(ctx, hipFreeAsync(a.clk, st));
+            unsigned long long t0 = ~0ull;
+            for (uint32_t q = 0; q < z.chain_grid; ++q)
+                t0 = h[8ull * q] < t0 ? h[8ull * q] : t0;
+            double mx[8] = {0}, av[8] = {0};
+            for (uint32_t q = 0; q < z.chain_grid; ++q)
+                for (int k = 0; k < 8; ++k) {
+                    const double v = (double) (h[8ull * q + k] - t0) / 100.0; // us (100 MHz)
+                    mx[k] = v > mx[k] ? v : mx[k];
+                    av[k] += v / z.chain_grid;
+                }
+            fprintf(stderr, "zmtp_chain us since first start (avg/max): start %.1f/%.1f p0a %.1f/%.1f b1 %.1f/%.1f "
+                            "p0b %.1f/%.1f b2 %.1f/%.1f links %.1f/%.1f b3 %.1f/%.1f frames %.1f/%.1f\n",
+                    av[0], mx[0], av[1], mx[1], av[2], mx[2], av[3], mx[3], av[4], mx[4], av[5], mx[5], av[6], mx[6],
+                    av[7], mx[7]);
+        }
+        zmqg_batch_opts o{};
+        o.size = sizeof o;
+        if (max_msg_size >= 0 && (uint64_t) max_msg_size <= kMaxFrameStream)
+            o.max_len = max_msg_size > 0 ? (uint64_t) max_msg_size : 1u;
+        return decode_batch_impl(ctx, max_frames, z.sid_fill, frame_in_off, frame_len, in, out_off, out, flags_out,
+                                 status_out, o.max_len ? &o : nullptr, z.fflags, stream);
+    }
     // persistent grids over device-side counts: enough workgroups to cover
     // config-2-sized streams in one pass
     const uint32_t pg = (uint32_t) (ctx->cus > 0 ? 4 * ctx->cus : 1024);
     const uint64_t *m_p = z.off_wg + nwg; // the candidate count, on the device
     // 1. candidates, in stream order: per-workgroup lists, their counts'
     // exclusive sum, the lists concatenated
-    hipLaunchKernelGGL(k_zmtp_scan, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
+    hipLaunchKernelGGL(zmtp_scan_kernel(), dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
                        z.count_wg);
     ZCHECK(ctx, hipGetLastError());
     if (nwg <= 8u * kZmtpScan1) {
@@ -3289,6 +3387,8 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
     // the one read back of the call
     ZCHECK(ctx, hipMemcpyAsync(result, ctx->zw.res, sizeof *result, hipMemcpyDeviceToHost, st));
     ZCHECK(ctx, hipStreamSynchronize(st));
+    if (result->error == ETIMEDOUT && ctx->zw.bar) // a barrier gave up: its counts start over
+        ZCHECK(ctx, hipMemsetAsync(ctx->zw.bar, 0, sizeof(ZmtpBar), st));
     return 0;
 }
 
