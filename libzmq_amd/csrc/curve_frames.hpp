@@ -354,6 +354,8 @@ struct FrameCtl {
                                    // counter; frame i takes *nonce_ctr + i, the last workgroup adds n
     uint64_t out_limit;  // (out_check) the caller's out_bytes: the staging area's extent
     const uint8_t *zflags; // decode from zmqg_decode_zmtp: each frame's ZMTP flags byte (or null)
+    const unsigned long long *res_src; // zmqg_decode_zmtp: 32 bytes workgroup 0 copies to res_dst at its end
+    unsigned long long *res_dst;       // (the call's result, from the parse state), or null
 };
 
 // msg_t flags a received ZMTP frame adds to its decoded message: the
@@ -448,6 +450,9 @@ __device__ __forceinline__ void call_state_end(ZState *zs, const FrameCtl &ctl, 
         __hip_atomic_store(&zs->epoch, c.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!DEC && ctl.nonce_ctr)
             __hip_atomic_store(ctl.nonce_ctr, c.nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ctl.res_src)
+            for (int k = 0; k < 4; ++k)
+                ctl.res_dst[k] = ctl.res_src[k];
     }
 }
 

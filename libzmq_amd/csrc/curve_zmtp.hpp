@@ -24,7 +24,7 @@
 //      stream order and concatenated (k_zmtp_scan, k_zmtp_compact);
 //   2. links: candidate k is linked when the frame at cand[k] ends exactly
 //      at cand[k+1]; each candidate learns the next unlinked one
-//      (k_zmtp_links, k_zmtp_segnext; normally only the last is unlinked);
+//      (k_zmtp_compact, k_zmtp_next_walk; normally only the last is unlinked);
 //   3. one thread walks the chain from offset 0 over whole linked runs,
 //      jumping only at unlinked candidates (a binary search for the next
 //      frame's offset among the candidates), and records the runs;
@@ -183,40 +183,6 @@ __device__ __forceinline__ uint64_t zmtp_block_excl4(uint64_t v, uint64_t &total
     return base + x - v;
 }
 
-// NB stream bytes at off (NB = 8 or 16) as words, zero outside [0, n)
-template <int NB>
-__device__ __forceinline__ void zmtp_load_words(const uint8_t *b, uint64_t n, int64_t off, uint32_t (&x)[NB / 4])
-{
-    if (off >= 0 && (uint64_t) off + NB <= n) {
-        if constexpr (NB == 16) {
-            const uint4 v = *(const uint4 *) (b + off);
-            x[0] = v.x;
-            x[1] = v.y;
-            x[2] = v.z;
-            x[3] = v.w;
-        } else {
-            const uint2 v = *(const uint2 *) (b + off);
-            x[0] = v.x;
-            x[1] = v.y;
-        }
-        return;
-    }
-#pragma unroll
-    for (int q = 0; q < NB / 4; ++q) {
-        uint32_t v = 0;
-        for (int j = 0; j < 4; ++j) {
-            const int64_t p = off + 4 * q + j;
-            v |= (uint32_t) (p >= 0 && (uint64_t) p < n ? b[p] : 0u) << (8 * j);
-        }
-        x[q] = v;
-    }
-}
-
-// SHFL (round 4): each lane loads only its own 16-byte chunk; the 16 bytes
-// before it and the 8 after come from the neighbouring lanes by shuffles,
-// lanes 0 and 63 load theirs (one coalesced load per chunk instead of three
-// overlapping ones).
-template <bool SHFL>
 __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, uint64_t n, int64_t max_msg,
                                                             uint64_t *cand_wg, uint64_t *count_wg)
 {
@@ -232,37 +198,6 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
     const uint64_t wg0 = (uint64_t) blockIdx.x * kZmtpWgBytes;
     uint64_t *const dst0 = cand_wg + (size_t) blockIdx.x * kZmtpWgCap;
     uint32_t w[R][10]; // round k: stream bytes [base_k - 16, base_k + 24), zero outside [0, n)
-    if (SHFL) {
-        const uint32_t lane = threadIdx.x & 63u;
-        uint32_t c[R][4];
-#pragma unroll
-        for (uint32_t k = 0; k < R; ++k)
-            zmtp_load_words<16>(b, n, (int64_t) (wg0 + 16ull * (k * kZmtpThreads + threadIdx.x)), c[k]);
-#pragma unroll
-        for (uint32_t k = 0; k < R; ++k) {
-            const int64_t base = (int64_t) (wg0 + 16ull * (k * kZmtpThreads + threadIdx.x));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                w[k][q] = (uint32_t) __shfl_up((int) c[k][q], 1);
-                w[k][4 + q] = c[k][q];
-            }
-            w[k][8] = (uint32_t) __shfl_down((int) c[k][0], 1);
-            w[k][9] = (uint32_t) __shfl_down((int) c[k][1], 1);
-            if (lane == 0) {
-                uint32_t p[4];
-                zmtp_load_words<16>(b, n, base - 16, p);
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    w[k][q] = p[q];
-            }
-            if (lane == 63) {
-                uint32_t p[2];
-                zmtp_load_words<8>(b, n, base + 16, p);
-                w[k][8] = p[0];
-                w[k][9] = p[1];
-            }
-        }
-    } else {
 #pragma unroll
     for (uint32_t k = 0; k < R; ++k) {
         const uint64_t base = wg0 + 16ull * (k * kZmtpThreads + threadIdx.x);
@@ -291,7 +226,6 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
                 w[k][q] = x;
             }
         }
-    }
     }
     uint64_t f[R][2]; // (at most 2 per chunk: signatures are >= 8 bytes apart)
     uint32_t cnt[R];
@@ -353,84 +287,81 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
 }
 
 // Workgroup lists -> the sorted candidate array (off_wg: exclusive sum of the
-// counts, off_wg[nwg] = m).
-__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint64_t *cand_wg, const uint64_t *count_wg,
-                                                               const uint64_t *off_wg, uint64_t *cand)
+// counts, off_wg[nwg] = m), and the links (round 4: in this kernel, no launch
+// of their own): candidate k is unlinked when its frame does not end at
+// candidate k+1 (the last one never does).  k+1 is the next entry of the same
+// list, or the first entry of the next non-empty list (nxt, from
+// k_zmtp_exsum), so no other workgroup's output is needed.  Per list: nb[k] =
+// the first unlinked index >= k in k's list (or none), first_w[w] = the first
+// unlinked index of list w (or none), wid[k] = w.
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint8_t *b, uint64_t n, const uint64_t *cand_wg,
+                                                               const uint64_t *count_wg, const uint64_t *off_wg,
+                                                               const uint32_t *nxt, uint32_t nwg, uint64_t *cand,
+                                                               uint64_t *nb, uint64_t *first_w, uint32_t *wid)
 {
-    const uint32_t w = blockIdx.x, c = (uint32_t) count_wg[w];
+    __shared__ unsigned long long sh[kZmtpThreads / 64];
+    const uint32_t w = blockIdx.x, c = (uint32_t) count_wg[w], tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
     const uint64_t o = off_wg[w];
-    for (uint32_t k = threadIdx.x; k < c; k += kZmtpThreads)
-        cand[o + k] = cand_wg[(size_t) w * kZmtpWgCap + k];
-}
-
-// Links: candidate k is unlinked when its frame does not end at candidate
-// k+1 (the last one never does).  Over segments of 256 candidates (a
-// persistent grid; m is read on the device): nb[k] = the first unlinked index
-// >= k inside k's segment (or none), first_seg[s] = nb of segment s's first
-// candidate.
-constexpr uint32_t kZmtpSeg = 256;
-__device__ __forceinline__ void zmtp_links_seg(const uint8_t *b, uint64_t n, const uint64_t *cand, uint64_t m,
-                                               uint64_t sg, uint64_t *nb, uint64_t *first_seg);
-__global__ __launch_bounds__(kZmtpSeg) void k_zmtp_links(const uint8_t *b, uint64_t n, const uint64_t *cand,
-                                                         const uint64_t *m_p, uint64_t *nb, uint64_t *first_seg)
-{
-    const uint64_t m = *m_p, nseg = (m + kZmtpSeg - 1) / kZmtpSeg;
-    for (uint64_t sg = blockIdx.x; sg < nseg; sg += gridDim.x)
-        zmtp_links_seg(b, n, cand, m, sg, nb, first_seg);
-}
-
-// Links of segment sg (256 threads, one candidate each): see k_zmtp_links.
-__device__ __forceinline__ void zmtp_links_seg(const uint8_t *b, uint64_t n, const uint64_t *cand, uint64_t m,
-                                               uint64_t sg, uint64_t *nb, uint64_t *first_seg)
-{
-    __shared__ unsigned long long sh[kZmtpSeg / 64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t k = sg * kZmtpSeg + threadIdx.x;
-    unsigned long long u = kZmtpNone;
-    if (k < m) {
-        bool unl = k + 1 >= m;
-        if (!unl) {
+    const uint64_t *const list = cand_wg + (size_t) w * kZmtpWgCap;
+    unsigned long long carry = kZmtpNone; // the minimum over the later chunks
+    for (int j = (int) ((c + kZmtpThreads - 1) / kZmtpThreads) - 1; j >= 0; --j) {
+        const uint32_t k = (uint32_t) j * kZmtpThreads + tid;
+        unsigned long long u = kZmtpNone;
+        if (k < c) {
+            const uint64_t p = list[k];
+            cand[o + k] = p;
+            wid[o + k] = w;
+            uint64_t next = kZmtpNone;
+            if (k + 1 < c)
+                next = list[k + 1];
+            else if (nxt[w] < nwg)
+                next = cand_wg[(size_t) nxt[w] * kZmtpWgCap];
             uint32_t hdr;
             uint64_t size;
-            zmtp_header(b, n, cand[k], hdr, size);
-            unl = cand[k + 1] != cand[k] + hdr + size;
+            zmtp_header(b, n, p, hdr, size);
+            u = next != p + hdr + size ? o + k : kZmtpNone;
         }
-        u = unl ? k : kZmtpNone;
-    }
-    // suffix minimum: within the wave, then over the later waves
+        // suffix minimum within the chunk, then the later chunks'
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long o = __shfl_down(u, d);
-        if (lane + d < 64u && o < u)
-            u = o;
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long x = __shfl_down(u, d);
+            if (lane + d < 64u && x < u)
+                u = x;
+        }
+        __syncthreads();
+        if (lane == 0)
+            sh[wv] = u;
+        __syncthreads();
+        for (uint32_t q = wv + 1; q < kZmtpThreads / 64; ++q)
+            u = sh[q] < u ? sh[q] : u;
+        u = carry < u ? carry : u;
+        if (k < c)
+            nb[o + k] = u;
+        // the chunk's minimum: wave 0's lane 0 value with the later waves' and chunks'
+        unsigned long long lo = carry;
+        for (uint32_t q = 0; q < kZmtpThreads / 64; ++q)
+            lo = sh[q] < lo ? sh[q] : lo;
+        carry = lo;
     }
-    if (lane == 0)
-        sh[wv] = u;
-    __syncthreads();
-    for (uint32_t q = wv + 1; q < kZmtpSeg / 64; ++q)
-        if (sh[q] < u)
-            u = sh[q];
-    if (k < m)
-        nb[k] = u;
-    if (threadIdx.x == 0)
-        first_seg[sg] = u;
-    __syncthreads();
+    if (tid == 0)
+        first_w[w] = carry;
 }
 
-// first_seg -> its suffix minimum over segments, in place (one workgroup of
-// T threads, each a contiguous run of segments): the first unlinked
-// candidate in segments >= s.
+// first_w -> its suffix minimum over the lists, in place (one workgroup of T
+// threads, each a contiguous run of entries): the first unlinked candidate in
+// lists >= w.
 constexpr uint32_t kZmtpNextThreads = 1024;
 template <uint32_t T>
-__device__ void zmtp_segnext(uint64_t *first_seg, uint64_t m)
+__device__ void zmtp_suffix_min(uint64_t *first_w, uint64_t count)
 {
     __shared__ unsigned long long sh[T];
-    const uint64_t nseg = (m + kZmtpSeg - 1) / kZmtpSeg;
-    const uint64_t per = (nseg + T - 1) / T;
-    const uint64_t r0 = threadIdx.x * per, r1 = r0 + per < nseg ? r0 + per : nseg;
+    const uint64_t per = (count + T - 1) / T;
+    const uint64_t r0 = threadIdx.x * per < count ? threadIdx.x * per : count;
+    const uint64_t r1 = r0 + per < count ? r0 + per : count;
     unsigned long long mn = kZmtpNone;
     for (uint64_t s = r0; s < r1; ++s)
-        mn = first_seg[s] < mn ? first_seg[s] : mn;
+        mn = first_w[s] < mn ? first_w[s] : mn;
     sh[threadIdx.x] = mn;
     __syncthreads();
     for (uint32_t d = 1; d < T; d <<= 1) {
@@ -442,21 +373,47 @@ __device__ void zmtp_segnext(uint64_t *first_seg, uint64_t m)
     }
     unsigned long long c = threadIdx.x + 1 < T ? sh[threadIdx.x + 1] : kZmtpNone;
     for (uint64_t s = r1; s-- > r0;) {
-        const unsigned long long x = first_seg[s];
+        const unsigned long long x = first_w[s];
         c = x < c ? x : c;
-        first_seg[s] = c;
+        first_w[s] = c;
     }
 }
 
 // Exclusive sum of v[0..n) into o[0..n] (o[n] = total) by one workgroup of
-// 1024 threads, each a contiguous run: the small scans of this path (the
-// workgroups' candidate counts; the frames' payload sizes) in one launch.
+// 1024 threads, each a contiguous run: the workgroups' candidate counts.
+// With nxt: nxt[i] = the first j > i with v[j] > 0, or n (the next non-empty
+// list, for k_zmtp_compact's links).
 constexpr uint32_t kZmtpScan1 = 1024;
-__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_exsum(const uint64_t *v, uint64_t n, uint64_t *o)
+__device__ void zmtp_next_nonempty(const uint64_t *v, uint64_t n, uint32_t *nxt)
 {
     __shared__ unsigned long long sh[kZmtpScan1];
     const uint64_t per = (n + kZmtpScan1 - 1) / kZmtpScan1;
-    const uint64_t r0 = threadIdx.x * per, r1 = r0 + per < n ? r0 + per : n;
+    const uint64_t r0 = threadIdx.x * per < n ? threadIdx.x * per : n, r1 = r0 + per < n ? r0 + per : n;
+    unsigned long long mn = n;
+    for (uint64_t i = r1; i-- > r0;)
+        mn = v[i] ? i : mn;
+    sh[threadIdx.x] = mn;
+    __syncthreads();
+    for (uint32_t d = 1; d < kZmtpScan1; d <<= 1) {
+        const unsigned long long o = threadIdx.x + d < kZmtpScan1 ? sh[threadIdx.x + d] : n;
+        __syncthreads();
+        if (o < sh[threadIdx.x])
+            sh[threadIdx.x] = o;
+        __syncthreads();
+    }
+    unsigned long long c = threadIdx.x + 1 < kZmtpScan1 ? sh[threadIdx.x + 1] : n;
+    for (uint64_t i = r1; i-- > r0;) {
+        nxt[i] = (uint32_t) c;
+        if (v[i])
+            c = i;
+    }
+}
+
+__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_exsum(const uint64_t *v, uint64_t n, uint64_t *o, uint32_t *nxt)
+{
+    __shared__ unsigned long long sh[kZmtpScan1];
+    const uint64_t per = (n + kZmtpScan1 - 1) / kZmtpScan1;
+    const uint64_t r0 = threadIdx.x * per < n ? threadIdx.x * per : n, r1 = r0 + per < n ? r0 + per : n;
     unsigned long long t = 0;
     for (uint64_t i = r0; i < r1; ++i)
         t += v[i];
@@ -476,28 +433,42 @@ __global__ __launch_bounds__(kZmtpScan1) void k_zmtp_exsum(const uint64_t *v, ui
     }
     if (threadIdx.x == kZmtpScan1 - 1)
         o[n] = sh[kZmtpScan1 - 1];
+    if (nxt) {
+        __syncthreads();
+        zmtp_next_nonempty(v, n, nxt);
+    }
 }
 
-// Parse state written by k_zmtp_walk (device).
+// nxt alone (streams whose counts hipCUB scans)
+__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_nxt(const uint64_t *v, uint64_t n, uint32_t *nxt)
+{
+    zmtp_next_nonempty(v, n, nxt);
+}
+
+// Parse state written by k_zmtp_walk (device).  It begins with the call's
+// result (zmqg_zmtp_result's layout), which the decode's frame kernel copies
+// to the caller's result (FrameCtl::res_src).
 struct ZmtpWalk {
-    unsigned long long frames;   // frames returned (chain + an extra last one)
-    unsigned long long consumed; // bytes of the buffer those frames cover
-    unsigned long long runs;     // linked runs on the chain
-    int32_t error;               // 0 or EMSGSIZE
-    uint32_t extra;              // 1: the last frame is a complete non-MESSAGE frame at `extra_off`
-    unsigned long long extra_off;
+    unsigned long long frames;    // frames returned (chain + an extra last one)
+    unsigned long long consumed;  // bytes of the buffer those frames cover
     unsigned long long out_bytes; // payload bytes of the returned frames (k_zmtp_frames adds them up)
+    int32_t error;                // 0 or EMSGSIZE
+    uint32_t pad;
+    unsigned long long runs;      // linked runs on the chain
+    uint32_t extra;               // 1: the last frame is a complete non-MESSAGE frame at `extra_off`
+    unsigned long long extra_off;
 };
+static_assert(sizeof(zmqg_zmtp_result) == 32 && offsetof(ZmtpWalk, runs) == 32, "the result prefix");
 
 // Thread 0 walks the chain (see the file comment).  run[2r], run[2r+1]: the
 // first and last candidate of run r; runpre[r]: frames before run r.  The
-// next unlinked candidate >= cur is nb[cur], or (none left in cur's
-// segment) first_seg[cur / kZmtpSeg + 1].
+// next unlinked candidate >= cur is nb[cur], or (none left in cur's list
+// wid[cur]) first_w[wid[cur] + 1], already a suffix minimum over the lists.
 __device__ void zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_t max_frames, const uint64_t *cand,
-                          const uint64_t *m_p, const uint64_t *nb, const uint64_t *first_seg, uint64_t *run,
-                          uint64_t *runpre, ZmtpWalk *out)
+                          const uint64_t *m_p, const uint64_t *nb, const uint64_t *first_w, const uint32_t *wid,
+                          uint64_t nwg, uint64_t *run, uint64_t *runpre, ZmtpWalk *out)
 {
-    const uint64_t m = *m_p, nseg = (m + kZmtpSeg - 1) / kZmtpSeg;
+    const uint64_t m = *m_p;
     uint64_t frames = 0, runs = 0, q = 0;
     bool full = false;
     if (m > 0 && cand[0] == 0 && max_frames > 0) {
@@ -505,8 +476,8 @@ __device__ void zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_
         for (;;) {
             uint64_t last = nb[cur];
             if (last == kZmtpNone) {
-                const uint64_t sg = cur / kZmtpSeg + 1u;
-                last = sg < nseg ? first_seg[sg] : kZmtpNone;
+                const uint64_t wn = (uint64_t) wid[cur] + 1u;
+                last = wn < nwg ? first_w[wn] : kZmtpNone;
             }
             if (last == kZmtpNone)
                 last = m - 1; // (the last candidate is always unlinked)
@@ -563,22 +534,22 @@ __device__ void zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_
     *out = w;
 }
 
-// first_seg's suffix minimum (k_zmtp_segnext), then thread 0 walks.
+// first_w's suffix minimum over the lists, then thread 0 walks.
 __global__ __launch_bounds__(kZmtpNextThreads) void k_zmtp_next_walk(const uint8_t *b, uint64_t n, int64_t max_msg,
                                                                      uint64_t max_frames, const uint64_t *cand,
                                                                      const uint64_t *m_p, const uint64_t *nb,
-                                                                     uint64_t *first_seg, uint64_t *run,
-                                                                     uint64_t *runpre, ZmtpWalk *out)
+                                                                     uint64_t *first_w, const uint32_t *wid,
+                                                                     uint64_t nwg, uint64_t *run, uint64_t *runpre,
+                                                                     ZmtpWalk *out)
 {
-    zmtp_segnext<kZmtpNextThreads>(first_seg, *m_p);
+    zmtp_suffix_min<kZmtpNextThreads>(first_w, nwg);
     __threadfence_block();
     __syncthreads();
     if (threadIdx.x == 0)
-        zmtp_walk(b, n, max_msg, max_frames, cand, m_p, nb, first_seg, run, runpre, out);
+        zmtp_walk(b, n, max_msg, max_frames, cand, m_p, nb, first_w, wid, nwg, run, runpre, out);
 }
 
-// Frame descriptors from the runs: one workgroup per candidate segment
-// (k_zmtp_links's layout).  Entries [frames, max_frames) get an empty frame
+// Frame descriptors from the runs (a persistent grid over the candidates).  Entries [frames, max_frames) get an empty frame
 // (offset 0, length 0: the decode reports it malformed and writes nothing
 // else), so the decode can run over max_frames without the frame count
 // reaching the host.
@@ -662,311 +633,6 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, 
 {
     zmtp_frames_body(b, n, cand, *m_p, run, runpre, walk, max_frames, f_off, f_len, f_flags, sid_fill, sid, out_off,
                      out_bytes, true);
-}
-
-// ---- the middle of the receive side in one launch (round 4)
-// k_zmtp_chain runs what k_zmtp_exsum, k_zmtp_compact, k_zmtp_links,
-// k_zmtp_next_walk and k_zmtp_frames do, separated by grid barriers, in one
-// launch of one workgroup per CU (far below what the device holds at once, so
-// every workgroup becomes resident while the others wait):
-//   P0a  empty descriptors over max_frames (so a decode after an abandoned
-//        launch reads only empty frames), each workgroup's share of the
-//        per-16-KiB candidate counts summed;
-//   --   barrier
-//   P0b  each workgroup's base = the sum of the shares before it, its counts
-//        scanned in LDS, its candidates copied into the sorted array;
-//   --   barrier
-//   P1   links per 256-candidate segment;
-//   --   barrier; the last workgroup to arrive takes the suffix minimum over
-//        segments and walks the chain before it releases the others
-//   P2   frame descriptors from the runs;
-//   the last workgroup to finish writes the call's result (frames,
-//   consumed, payload bytes, error).
-// A barrier gives up after ~200 ms (s_memrealtime ticks at 100 MHz): that
-// workgroup leaves, and the result keeps the ETIMEDOUT its first phase put
-// there.  The MORE / COMMAND bits of each frame are ORed into flags_out by
-// the decode itself (FrameCtl::zflags), so no flags launch follows.
-// Arrivals go through kZmtpBarGroups counters (workgroup b at b mod
-// kZmtpBarGroups), whose last arrivals meet at the top counter: same-address
-// device-scope atomics serialise (~20 ns each), so 256 arrivals at one word
-// cost ~6 us a barrier, through 16 + 16 ~1 us.  Each word sits on a cache
-// line of its own, so arrivals do not queue behind the polls of gen.
-constexpr uint32_t kZmtpBarGroups = 16;
-struct ZmtpBar {
-    struct alignas(256) Word {
-        unsigned int v;
-    };
-    Word sub[kZmtpBarGroups]; // workgroups of each group arrived at the current barrier
-    Word count;               // groups complete at the current barrier
-    Word gen;                 // barriers completed
-};
-
-struct ZmtpChainArgs {
-    const uint8_t *b;
-    uint64_t n;
-    int64_t max_msg;
-    uint64_t max_frames;
-    const uint64_t *cand_wg;
-    const uint64_t *count_wg;
-    uint64_t nwg;
-    uint64_t *off_wg; // off_wg[nwg] = the candidate count (m_p of the other kernels)
-    unsigned long long *part;
-    uint64_t *cand, *nb, *first_seg, *run, *runpre;
-    ZmtpWalk *walk;
-    uint64_t *f_off;
-    uint32_t *f_len;
-    uint8_t *f_flags;
-    uint32_t *sid_fill;
-    uint32_t sid;
-    uint64_t *out_off;
-    ZmtpBar *bar;
-    zmqg_zmtp_result *res;
-    unsigned long long *clk; // diagnostics (ZMQG_ZMTP_CLK): 8 s_memrealtime stamps per workgroup, or null
-};
-
-constexpr unsigned long long kZmtpBarTicks = 20000000ull; // 200 ms of s_memrealtime
-
-// Thread 0: count this workgroup in (two levels); true for the last one of
-// the grid.  The caller resets count when it is done with it.
-__device__ __forceinline__ bool zmtp_count_in(ZmtpBar *bar)
-{
-    const uint32_t G = gridDim.x, grp = blockIdx.x % kZmtpBarGroups;
-    const uint32_t ng = G < kZmtpBarGroups ? G : kZmtpBarGroups;
-    const uint32_t gsize = (G - grp + kZmtpBarGroups - 1) / kZmtpBarGroups;
-    const unsigned int c = __hip_atomic_fetch_add(&bar->sub[grp].v, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (c + 1u != gsize)
-        return false;
-    __hip_atomic_store(&bar->sub[grp].v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int c2 = __hip_atomic_fetch_add(&bar->count.v, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    return c2 + 1u == ng;
-}
-
-// Arrive at a barrier: true for the last workgroup to arrive (which must call
-// zmtp_release when it is done), after waiting for that release otherwise;
-// ok = false when the wait gave up.
-__device__ __forceinline__ bool zmtp_arrive(ZmtpBar *bar, bool &ok)
-{
-    __shared__ uint32_t sh_state; // 0 released, 1 last, 2 gave up
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); // the workgroup's writes of the phase
-        const unsigned int g = __hip_atomic_load(&bar->gen.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t s = 0;
-        if (zmtp_count_in(bar)) {
-            s = 1;
-        } else {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(&bar->gen.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-                __builtin_amdgcn_s_sleep(8); // (~512 cycles between polls)
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kZmtpBarTicks) {
-                    s = 2;
-                    break;
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        sh_state = s;
-    }
-    __syncthreads();
-    ok = sh_state != 2;
-    return sh_state == 1;
-}
-
-__device__ __forceinline__ void zmtp_release(ZmtpBar *bar)
-{
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&bar->count.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&bar->gen.v, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-__device__ __forceinline__ bool zmtp_grid_sync(ZmtpBar *bar)
-{
-    bool ok;
-    if (zmtp_arrive(bar, ok))
-        zmtp_release(bar);
-    return ok;
-}
-
-// sum over the workgroup (every thread gets it)
-__device__ __forceinline__ unsigned long long zmtp_block_sum(unsigned long long v)
-{
-    __shared__ unsigned long long sh[kZmtpThreads / 64];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1)
-        v += __shfl_xor(v, d);
-    __syncthreads();
-    if ((threadIdx.x & 63u) == 0)
-        sh[threadIdx.x >> 6] = v;
-    __syncthreads();
-    unsigned long long t = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < kZmtpThreads / 64; ++q)
-        t += sh[q];
-    return t;
-}
-
-__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_chain(ZmtpChainArgs a)
-{
-    const uint32_t G = gridDim.x, wb = blockIdx.x, tid = threadIdx.x;
-    const uint64_t stride = (uint64_t) G * kZmtpThreads;
-    auto stamp = [&](int k) {
-        if (a.clk && tid == 0)
-            a.clk[8ull * wb + k] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
-    // P0a
-    if (wb == 0 && tid == 0) {
-        zmqg_zmtp_result r{};
-        r.error = ETIMEDOUT; // replaced by the last workgroup unless a barrier gives up
-        *a.res = r;
-    }
-    for (uint64_t j = (uint64_t) wb * kZmtpThreads + tid; j < a.max_frames; j += stride) {
-        a.sid_fill[j] = a.sid;
-        a.f_off[j] = 0;
-        a.f_len[j] = 0;
-        a.f_flags[j] = 0;
-        a.out_off[j] = 0;
-    }
-    const uint64_t per = (a.nwg + G - 1) / G;
-    const uint64_t r0 = (uint64_t) wb * per < a.nwg ? (uint64_t) wb * per : a.nwg;
-    const uint64_t r1 = r0 + per < a.nwg ? r0 + per : a.nwg;
-    unsigned long long s = 0;
-    for (uint64_t w = r0 + tid; w < r1; w += kZmtpThreads)
-        s += a.count_wg[w];
-    s = zmtp_block_sum(s);
-    if (tid == 0)
-        a.part[wb] = s;
-    stamp(1);
-    if (!zmtp_grid_sync(a.bar))
-        return;
-    stamp(2);
-    // P0b: base and total from the shares, then the copies
-    unsigned long long before = 0, all = 0;
-    for (uint32_t q = tid; q < G; q += kZmtpThreads) {
-        const unsigned long long v = a.part[q];
-        all += v;
-        before += q < wb ? v : 0ull;
-    }
-    before = zmtp_block_sum(before);
-    const uint64_t m = zmtp_block_sum(all);
-    if (wb == 0 && tid == 0)
-        a.off_wg[a.nwg] = m;
-    __shared__ unsigned long long sh_off[kZmtpThreads + 1];
-    unsigned long long base = before;
-    for (uint64_t c0 = r0; c0 < r1; c0 += kZmtpThreads) {
-        // this chunk's counts, scanned in LDS
-        const uint64_t w = c0 + tid;
-        const unsigned long long cnt = w < r1 ? a.count_wg[w] : 0ull;
-        unsigned long long x = cnt;
-        const uint32_t lane = tid & 63u, wv = tid >> 6;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const unsigned long long o = __shfl_up(x, d);
-            if ((int) lane >= d)
-                x += o;
-        }
-        __shared__ unsigned long long sh_w[kZmtpThreads / 64];
-        __syncthreads();
-        if (lane == 63)
-            sh_w[wv] = x;
-        __syncthreads();
-        unsigned long long wbase = 0, tot = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kZmtpThreads / 64; ++q) {
-            wbase += q < wv ? sh_w[q] : 0ull;
-            tot += sh_w[q];
-        }
-        sh_off[tid] = wbase + x - cnt; // exclusive, within the chunk
-        if (tid == 0)
-            sh_off[kZmtpThreads] = tot;
-        __syncthreads();
-        const uint32_t nw = (uint32_t) (r1 - c0 < kZmtpThreads ? r1 - c0 : kZmtpThreads);
-        // copy item q of the chunk: the count slot holding it by binary search
-        for (unsigned long long q = tid; q < tot; q += kZmtpThreads) {
-            uint32_t lo = 0, hi = nw;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (sh_off[mid] <= q)
-                    lo = mid;
-                else
-                    hi = mid;
-            }
-            a.cand[base + q] = a.cand_wg[(size_t) (c0 + lo) * kZmtpWgCap + (q - sh_off[lo])];
-        }
-        base += tot;
-        __syncthreads();
-    }
-    stamp(3);
-    if (!zmtp_grid_sync(a.bar))
-        return;
-    stamp(4);
-    // P1: links
-    const uint64_t nseg = (m + kZmtpSeg - 1) / kZmtpSeg;
-    for (uint64_t sg = wb; sg < nseg; sg += G)
-        zmtp_links_seg(a.b, a.n, a.cand, m, sg, a.nb, a.first_seg);
-    stamp(5);
-    bool ok;
-    if (zmtp_arrive(a.bar, ok)) {
-        // the last to arrive: suffix minimum over segments, then the walk
-        zmtp_segnext<kZmtpThreads>(a.first_seg, m);
-        __threadfence_block();
-        __syncthreads();
-        if (tid == 0)
-            zmtp_walk(a.b, a.n, a.max_msg, a.max_frames, a.cand, a.off_wg + a.nwg, a.nb, a.first_seg, a.run,
-                      a.runpre, a.walk);
-        zmtp_release(a.bar);
-    } else if (!ok) {
-        return;
-    }
-    stamp(6);
-    // P2: descriptors of the chain's frames (the padding was P0a's)
-    zmtp_frames_body(a.b, a.n, a.cand, m, a.run, a.runpre, a.walk, a.max_frames, a.f_off, a.f_len, a.f_flags,
-                     a.sid_fill, a.sid, a.out_off, (unsigned long long *) &a.walk->out_bytes, false);
-    stamp(7);
-    // the last workgroup writes the result
-    __shared__ uint32_t sh_last;
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        sh_last = zmtp_count_in(a.bar);
-        if (sh_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __hip_atomic_store(&a.bar->count.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const ZmtpWalk w = *a.walk;
-            zmqg_zmtp_result r{};
-            r.frames = w.frames;
-            r.consumed = w.consumed;
-            r.error = w.error;
-            r.out_bytes = __hip_atomic_load((unsigned long long *) &a.walk->out_bytes, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-            *a.res = r;
-        }
-    }
-}
-
-// msg_t flags of a decoded frame: the ZMTP frame's MORE / COMMAND bits
-// (src/v2_decoder.cpp:35-41) ORed with the plaintext's (set_flags ORs,
-// src/msg.cpp:433-436); 0 for a frame that failed.
-// (and, thread 0, the call's result: frames, bytes consumed, payload
-// bytes, error -- one read back, or none for the asynchronous form)
-__global__ void k_zmtp_flags(const ZmtpWalk *walk, uint64_t max_frames, const uint8_t *f_flags, const int32_t *status,
-                             uint8_t *flags_out, zmqg_zmtp_result *res)
-{
-    const uint64_t j = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (j == 0) {
-        zmqg_zmtp_result r{};
-        r.frames = walk->frames;
-        r.consumed = walk->consumed;
-        r.error = walk->error;
-        r.out_bytes = walk->out_bytes;
-        *res = r;
-    }
-    if (j >= max_frames || j >= walk->frames || status[j] != 0)
-        return;
-    const uint8_t z = f_flags[j];
-    flags_out[j] |= (uint8_t) (((z & kZmtpMore) ? 1u : 0u) | ((z & kZmtpCommand) ? 2u : 0u));
 }
 
 // Send side: bytes of each frame (header + encoded body); F[n] = 0 so the

@@ -172,16 +172,15 @@ struct ZmtpWs {
     uint64_t *off_wg = nullptr;           // [g_cap + 1] exclusive sum of count_wg
     uint64_t *cand = nullptr;             // [c_cap] sorted candidates
     uint64_t *nb = nullptr;               // [c_cap] next unlinked candidate in the 256-candidate segment
-    uint64_t *first_seg = nullptr;        // [c_cap / 256 + 1] first unlinked candidate in segments >= s
+    uint64_t *first_w = nullptr;          // [g_cap + 1] first unlinked candidate in workgroup lists >= w
+    uint32_t *nxt = nullptr;              // [g_cap + 1] next non-empty workgroup list
+    uint32_t *wid = nullptr;              // [c_cap] each candidate's workgroup list
     uint64_t *run = nullptr;              // [2 (f_cap + 1)]
     uint64_t *runpre = nullptr;           // [f_cap + 1]
     uint32_t *sid_fill = nullptr;         // [f_cap]
     uint8_t *fflags = nullptr;            // [f_cap]
     ZmtpWalk *walk = nullptr;
     zmqg_zmtp_result *res = nullptr;      // the synchronous call's result on the device
-    ZmtpBar *bar = nullptr;               // k_zmtp_chain's grid barrier (zeroed once)
-    unsigned long long *part = nullptr;   // [chain_grid] k_zmtp_chain's per-workgroup count shares
-    uint32_t chain_grid = 0;              // k_zmtp_chain's workgroups (0: not yet sized; ~0u: no cooperative launch)
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };
@@ -2340,8 +2339,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
             (void) hipFree(p);
     {
         ZmtpWs &z = ctx->zw;
-        void *zp[] = {z.F,      z.wire_off, z.cand_wg,  z.count_wg, z.off_wg, z.cand, z.nb,  z.first_seg, z.run,
-                      z.runpre, z.sid_fill, z.fflags,   z.walk,     z.res,    z.temp};
+        void *zp[] = {z.F,      z.wire_off, z.cand_wg, z.count_wg, z.off_wg, z.cand, z.nb,   z.first_w, z.nxt,
+                      z.wid,    z.run,      z.runpre,  z.sid_fill, z.fflags, z.walk, z.res,  z.temp};
         for (void *p : zp)
             if (p)
                 (void) hipFree(p);
@@ -2695,7 +2694,7 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
 static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
                              const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
                              uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts,
-                             const uint8_t *zflags, void *stream)
+                             const uint8_t *zflags, const ZmtpWalk *zwalk, zmqg_zmtp_result *zres, void *stream)
 {
     if (!ctx || check_n(n) || check_opts(opts))
         return -EINVAL;
@@ -2734,6 +2733,8 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     FrameCtl ctl{};
     ctl.post = w.post;
     ctl.zflags = zflags;
+    ctl.res_src = (const unsigned long long *) zwalk;
+    ctl.res_dst = (unsigned long long *) zres;
     unsigned long long *smax = nullptr;
     if (opts) {
         ctl.max_len = opts->max_len;
@@ -2807,7 +2808,7 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
                          uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts, void *stream)
 {
     return decode_batch_impl(ctx, n, sid, in_off, wire_len, in, out_off, out, flags_out, status_out, opts, nullptr,
-                             stream);
+                             nullptr, nullptr, stream);
 }
 
 int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
@@ -3175,14 +3176,6 @@ int zmqg_encode_zmtp(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint6
     return zmqg_encode_batch(ctx, n, sid, nonce, flags, in_off, len, in, z.wire_off, out, stream);
 }
 
-// the candidate scan: the shuffle form unless ZMQG_ZMTP_SCAN1 is set (the
-// three-load form, kept for A/B runs)
-static void (*zmtp_scan_kernel())(const uint8_t *, uint64_t, int64_t, uint64_t *, uint64_t *)
-{
-    static const bool one = getenv("ZMQG_ZMTP_SCAN1") != nullptr;
-    return one ? k_zmtp_scan<false> : k_zmtp_scan<true>;
-}
-
 int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
                            uint64_t max_frames, uint64_t *frame_in_off, uint32_t *frame_len, uint64_t *out_off,
                            uint8_t *out, uint8_t *flags_out, int32_t *status_out, zmqg_zmtp_result *result,
@@ -3207,7 +3200,8 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         while (cap < nwg)
             cap *= 2;
         if ((rc = grow(ctx, z.cand_wg, cap * kZmtpWgCap, st)) || (rc = grow(ctx, z.count_wg, cap + 1, st)) ||
-            (rc = grow(ctx, z.off_wg, cap + 1, st)))
+            (rc = grow(ctx, z.off_wg, cap + 1, st)) || (rc = grow(ctx, z.first_w, cap + 1, st)) ||
+            (rc = grow(ctx, z.nxt, cap + 1, st)))
             return rc;
         z.g_cap = cap;
     }
@@ -3217,8 +3211,7 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         uint64_t cap = z.c_cap ? z.c_cap : 1024;
         while (cap < ccap)
             cap *= 2;
-        if ((rc = grow(ctx, z.cand, cap, st)) || (rc = grow(ctx, z.nb, cap, st)) ||
-            (rc = grow(ctx, z.first_seg, cap / kZmtpSeg + 2, st)))
+        if ((rc = grow(ctx, z.cand, cap, st)) || (rc = grow(ctx, z.nb, cap, st)) || (rc = grow(ctx, z.wid, cap, st)))
             return rc;
         z.c_cap = cap;
     }
@@ -3234,93 +3227,20 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
     if (!z.walk && (rc = grow(ctx, z.walk, 1, st)))
         return rc;
     const uint32_t g = (uint32_t) nwg;
-    // The middle in one launch (k_zmtp_chain, one workgroup per CU, grid
-    // barriers) unless the device cannot hold that grid at once or
-    // ZMQG_ZMTP_SPLIT is set (the separate launches below, kept for A/B runs).
-    if (!z.chain_grid) {
-        int nb = 0;
-        ZCHECK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_zmtp_chain, kZmtpThreads, 0));
-        const int cus = ctx->cus > 0 ? ctx->cus : 1;
-        z.chain_grid = nb > 0 && getenv("ZMQG_ZMTP_SPLIT") == nullptr ? (uint32_t) cus : ~0u;
-        if (z.chain_grid != ~0u) {
-            if ((rc = grow(ctx, z.bar, 1, st)) || (rc = grow(ctx, z.part, z.chain_grid, st)))
-                return rc;
-            ZCHECK(ctx, hipMemsetAsync(z.bar, 0, sizeof(ZmtpBar), st));
-        }
-    }
-    const bool chain = z.chain_grid != ~0u;
-    if (chain) {
-        hipLaunchKernelGGL(zmtp_scan_kernel(), dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
-                           z.count_wg);
-        ZCHECK(ctx, hipGetLastError());
-        ZmtpChainArgs a{};
-        a.b = in;
-        a.n = in_bytes;
-        a.max_msg = max_msg_size;
-        a.max_frames = max_frames;
-        a.cand_wg = z.cand_wg;
-        a.count_wg = z.count_wg;
-        a.nwg = nwg;
-        a.off_wg = z.off_wg;
-        a.part = z.part;
-        a.cand = z.cand;
-        a.nb = z.nb;
-        a.first_seg = z.first_seg;
-        a.run = z.run;
-        a.runpre = z.runpre;
-        a.walk = z.walk;
-        a.f_off = frame_in_off;
-        a.f_len = frame_len;
-        a.f_flags = z.fflags;
-        a.sid_fill = z.sid_fill;
-        a.sid = sid;
-        a.out_off = out_off;
-        a.bar = z.bar;
-        a.res = result;
-        static const bool clk = getenv("ZMQG_ZMTP_CLK") != nullptr; // diagnostics: phase times to stderr
-        if (clk)
-            ZCHECK(ctx, hipMallocAsync((void **) &a.clk, 8ull * z.chain_grid * sizeof(unsigned long long), st));
-        hipLaunchKernelGGL(k_zmtp_chain, dim3(z.chain_grid), dim3(kZmtpThreads), 0, st, a);
-        ZCHECK(ctx, hipGetLastError());
-        if (clk) {
-            std::vector<unsigned long long> h(8ull * z.chain_grid);
-            ZCHECK(ctx, hipMemcpyAsync(h.data(), a.clk, h.size() * 8, hipMemcpyDeviceToHost, st));
-            ZCHECK(ctx, hipStreamSynchronize(st));
-            ZCHECK(ctx, hipFreeAsync(a.clk, st));
-            unsigned long long t0 = ~0ull;
-            for (uint32_t q = 0; q < z.chain_grid; ++q)
-                t0 = h[8ull * q] < t0 ? h[8ull * q] : t0;
-            double mx[8] = {0}, av[8] = {0};
-            for (uint32_t q = 0; q < z.chain_grid; ++q)
-                for (int k = 0; k < 8; ++k) {
-                    const double v = (double) (h[8ull * q + k] - t0) / 100.0; // us (100 MHz)
-                    mx[k] = v > mx[k] ? v : mx[k];
-                    av[k] += v / z.chain_grid;
-                }
-            fprintf(stderr, "zmtp_chain us since first start (avg/max): start %.1f/%.1f p0a %.1f/%.1f b1 %.1f/%.1f "
-                            "p0b %.1f/%.1f b2 %.1f/%.1f links %.1f/%.1f b3 %.1f/%.1f frames %.1f/%.1f\n",
-                    av[0], mx[0], av[1], mx[1], av[2], mx[2], av[3], mx[3], av[4], mx[4], av[5], mx[5], av[6], mx[6],
-                    av[7], mx[7]);
-        }
-        zmqg_batch_opts o{};
-        o.size = sizeof o;
-        if (max_msg_size >= 0 && (uint64_t) max_msg_size <= kMaxFrameStream)
-            o.max_len = max_msg_size > 0 ? (uint64_t) max_msg_size : 1u;
-        return decode_batch_impl(ctx, max_frames, z.sid_fill, frame_in_off, frame_len, in, out_off, out, flags_out,
-                                 status_out, o.max_len ? &o : nullptr, z.fflags, stream);
-    }
     // persistent grids over device-side counts: enough workgroups to cover
     // config-2-sized streams in one pass
     const uint32_t pg = (uint32_t) (ctx->cus > 0 ? 4 * ctx->cus : 1024);
     const uint64_t *m_p = z.off_wg + nwg; // the candidate count, on the device
     // 1. candidates, in stream order: per-workgroup lists, their counts'
-    // exclusive sum, the lists concatenated
-    hipLaunchKernelGGL(zmtp_scan_kernel(), dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
+    // exclusive sum (and each list's next non-empty one), the lists
+    // concatenated with their links
+    hipLaunchKernelGGL(k_zmtp_scan, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
                        z.count_wg);
     ZCHECK(ctx, hipGetLastError());
-    if (nwg <= 8u * kZmtpScan1) {
+    // (ZMQG_ZMTP_CUB: the large-stream form at any size, for its tests)
+    if (nwg <= 8u * kZmtpScan1 && !getenv("ZMQG_ZMTP_CUB")) {
         hipLaunchKernelGGL(k_zmtp_exsum, dim3(1), dim3(kZmtpScan1), 0, st, (const uint64_t *) z.count_wg, nwg,
-                           z.off_wg);
+                           z.off_wg, z.nxt);
         ZCHECK(ctx, hipGetLastError());
     } else {
         size_t need = 0;
@@ -3330,20 +3250,19 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         ZCHECK(ctx, hipMemsetAsync(z.count_wg + nwg, 0, sizeof(uint64_t), st));
         size_t tb = z.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.count_wg, z.off_wg, (int) (nwg + 1), st));
+        hipLaunchKernelGGL(k_zmtp_nxt, dim3(1), dim3(kZmtpScan1), 0, st, (const uint64_t *) z.count_wg, nwg, z.nxt);
+        ZCHECK(ctx, hipGetLastError());
     }
-    hipLaunchKernelGGL(k_zmtp_compact, dim3(g), dim3(kZmtpThreads), 0, st, (const uint64_t *) z.cand_wg,
-                       (const uint64_t *) z.count_wg, (const uint64_t *) z.off_wg, z.cand);
+    hipLaunchKernelGGL(k_zmtp_compact, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand_wg,
+                       (const uint64_t *) z.count_wg, (const uint64_t *) z.off_wg, (const uint32_t *) z.nxt, g, z.cand,
+                       z.nb, z.first_w, z.wid);
     ZCHECK(ctx, hipGetLastError());
-    // 2. links
-    hipLaunchKernelGGL(k_zmtp_links, dim3(pg), dim3(kZmtpSeg), 0, st, in, in_bytes, (const uint64_t *) z.cand, m_p,
-                       z.nb, z.first_seg);
-    ZCHECK(ctx, hipGetLastError());
-    // 3. the next unlinked candidate per segment, then the walk (one launch)
+    // 2. the first unlinked candidate after each list, then the walk (one launch)
     hipLaunchKernelGGL(k_zmtp_next_walk, dim3(1), dim3(kZmtpNextThreads), 0, st, in, in_bytes, max_msg_size,
-                       max_frames, (const uint64_t *) z.cand, m_p, (const uint64_t *) z.nb, z.first_seg, z.run,
-                       z.runpre, z.walk);
+                       max_frames, (const uint64_t *) z.cand, m_p, (const uint64_t *) z.nb, z.first_w,
+                       (const uint32_t *) z.wid, nwg, z.run, z.runpre, z.walk);
     ZCHECK(ctx, hipGetLastError());
-    // 4. descriptors (empty frames up to max_frames); each payload goes to
+    // 3. descriptors (empty frames up to max_frames); each payload goes to
     // its body's offset in `out`, so no offsets scan is needed
     hipLaunchKernelGGL(k_zmtp_frames, dim3(pg), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand, m_p,
                        (const uint64_t *) z.run, (const uint64_t *) z.runpre, (const ZmtpWalk *) z.walk, max_frames,
@@ -3357,15 +3276,10 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
     o.size = sizeof o;
     if (max_msg_size >= 0 && (uint64_t) max_msg_size <= kMaxFrameStream)
         o.max_len = max_msg_size > 0 ? (uint64_t) max_msg_size : 1u;
-    rc = zmqg_decode_batch_ex(ctx, max_frames, z.sid_fill, frame_in_off, frame_len, in, out_off, out, flags_out,
-                              status_out, o.max_len ? &o : nullptr, stream);
-    if (rc)
-        return rc;
-    hipLaunchKernelGGL(k_zmtp_flags, dim3((unsigned) ((max_frames + 255) / 256)), dim3(256), 0, st,
-                       (const ZmtpWalk *) z.walk, max_frames, (const uint8_t *) z.fflags, (const int32_t *) status_out,
-                       flags_out, result);
-    ZCHECK(ctx, hipGetLastError());
-    return 0;
+    // (the frames' MORE / COMMAND bits ORed into flags_out, and the call's
+    // result copied from the parse state, by the decode's frame kernel)
+    return decode_batch_impl(ctx, max_frames, z.sid_fill, frame_in_off, frame_len, in, out_off, out, flags_out,
+                             status_out, o.max_len ? &o : nullptr, z.fflags, z.walk, result, stream);
 }
 
 int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in_bytes, int64_t max_msg_size,
@@ -3387,8 +3301,6 @@ int zmqg_decode_zmtp(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint64_t in
     // the one read back of the call
     ZCHECK(ctx, hipMemcpyAsync(result, ctx->zw.res, sizeof *result, hipMemcpyDeviceToHost, st));
     ZCHECK(ctx, hipStreamSynchronize(st));
-    if (result->error == ETIMEDOUT && ctx->zw.bar) // a barrier gave up: its counts start over
-        ZCHECK(ctx, hipMemsetAsync(ctx->zw.bar, 0, sizeof(ZmtpBar), st));
     return 0;
 }
 

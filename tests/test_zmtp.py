@@ -74,7 +74,11 @@ def test_encode_zmtp_matches_oracle(torch_cuda, C):
 
 def _stream_case(rng, case, precom, n=400):
     """A received byte stream of one connection and the decoder settings."""
-    b = random_batch(rng, n, [0, 5, 100, 222, 223, 1024, 3000], 1, flag_choices=(0, 1, 2))
+    if case == "sparse":  # large frames: most 16 KiB scan lists hold no candidate
+        n = 60
+        b = random_batch(rng, n, [100, 40000, 70000], 1, flag_choices=(0, 1, 2))
+    else:
+        b = random_batch(rng, n, [0, 5, 100, 222, 223, 1024, 3000], 1, flag_choices=(0, 1, 2))
     sessions = O.make_sessions([precom])
     out_off, wl, wtotal = wire_layout(b["flags"], b["lens"], [False], b["sid"])
     wire = O.encode_batch(sessions, b["sid"], b["nonce"], b["flags"], b["in_off"], b["lens"], b["inp"], out_off, wtotal)
@@ -118,11 +122,17 @@ def _stream_case(rng, case, precom, n=400):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["clean", "truncated", "planted", "flood", "large_small", "ping", "emsgsize",
-                                  "max_frames", "zmtp_flags"])
-def test_decode_zmtp_matches_oracle(torch_cuda, C, case):
+                                  "max_frames", "zmtp_flags", "sparse", "planted+cub", "sparse+cub"])
+def test_decode_zmtp_matches_oracle(torch_cuda, C, case, monkeypatch):
+    """+cub: the candidate counts scanned by hipCUB (the form for streams above
+    128 MiB, ZMQG_ZMTP_CUB forces it) with the next-non-empty-list pass of its
+    own launch."""
     torch = torch_cuda
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(zlib.crc32(case.encode()))
+    if case.endswith("+cub"):
+        monkeypatch.setenv("ZMQG_ZMTP_CUB", "1")
+        case = case[:-4]
     precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     stream, max_msg, max_frames = _stream_case(rng, case, precom)
     ref = Z.parse(stream, max_msg, max_frames)
@@ -191,7 +201,7 @@ def test_decode_zmtp_matches_oracle(torch_cuda, C, case):
         for i in range(nf):
             a, p0, ln = int(f_off[i]), int(p_off[i]), int(plen[i])
             assert got[a:a + ln].tobytes() == pl[p0:p0 + ln].tobytes(), i
-    if case in ("clean", "large_small", "zmtp_flags"):
+    if case in ("clean", "large_small", "zmtp_flags", "sparse"):
         assert (st == 0).all() and ref["consumed"] == len(stream)
     if case in ("planted", "flood"):
         assert (st == C.ERR_CRYPTOGRAPHIC).any() and ref["consumed"] == len(stream)
