@@ -353,9 +353,6 @@ struct FrameCtl {
     unsigned long long *nonce_ctr; // encode, one session, ZMQG_OPT_NONCE_AUTO: the session's send
                                    // counter; frame i takes *nonce_ctr + i, the last workgroup adds n
     uint64_t out_limit;  // (out_check) the caller's out_bytes: the staging area's extent
-    const uint8_t *zflags; // decode from zmqg_decode_zmtp: each frame's ZMTP flags byte (or null)
-    const unsigned long long *res_src; // zmqg_decode_zmtp: 32 bytes workgroup 0 copies to res_dst at its end
-    unsigned long long *res_dst;       // (the call's result, from the parse state), or null
 };
 
 // msg_t flags a received ZMTP frame adds to its decoded message: the
@@ -367,6 +364,29 @@ __device__ __forceinline__ uint32_t zmtp_msg_bits(const uint8_t *zflags, uint32_
         return 0u;
     const uint32_t z = zflags[i];
     return (z & 1u) | ((z & 4u) ? 2u : 0u); // ZMTP MORE (1) / COMMAND (4) -> msg_t more (1) / command (2)
+}
+
+// zmqg_decode_zmtp's two additions to a decode, carried by the decode's
+// BigOp (DecodeHead: zflags, res_src, res_dst) so that the encode kernels do
+// not change: the frames' ZMTP flag bits, and the call's result copied from
+// the parse state by one thread of workgroup 0.
+template <bool DEC, class BigOp>
+__device__ __forceinline__ uint32_t frame_zbits(const BigOp &big, uint32_t i)
+{
+    if constexpr (DEC)
+        return zmtp_msg_bits(big.zflags, i);
+    else
+        return 0u;
+}
+
+template <bool DEC, class BigOp>
+__device__ __forceinline__ void frame_result_copy(const BigOp &big)
+{
+    if constexpr (DEC) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && big.res_src)
+            for (int k = 0; k < 4; ++k)
+                big.res_dst[k] = big.res_src[k];
+    }
 }
 
 // A frame the call must not process (status ZMQG_ERR_BOUND, nothing
@@ -450,9 +470,6 @@ __device__ __forceinline__ void call_state_end(ZState *zs, const FrameCtl &ctl, 
         __hip_atomic_store(&zs->epoch, c.epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!DEC && ctl.nonce_ctr)
             __hip_atomic_store(ctl.nonce_ctr, c.nbase + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (ctl.res_src)
-            for (int k = 0; k < 4; ++k)
-                ctl.res_dst[k] = ctl.res_src[k];
     }
 }
 
@@ -982,6 +999,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
                __builtin_amdgcn_s_getreg((31 << 11) | 4); // XCC_ID : HW_ID
     }
     call_state_end<DEC>(zs, ctl, cs, n);
+    frame_result_copy<DEC>(big);
     if (!DEC && valid && q == 0 && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
     if (!valid || q != 0 || !small)
@@ -1006,7 +1024,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
         else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
         status_out[i] = status;
-        flags_out[i] = status == 0 ? (uint8_t) (fl | zmtp_msg_bits(ctl.zflags, i)) : 0;
+        flags_out[i] = status == 0 ? (uint8_t) (fl | frame_zbits<DEC>(big, i)) : 0;
         if (status != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the group's plaintext stores first
             zero_bytes(dst, S - 33u);
@@ -1578,6 +1596,7 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
         big(i, list_ctr, nbase);
     }
     call_state_end<DEC>(zs, ctl, cs, n);
+    frame_result_copy<DEC>(big);
     SEQ_STAMP(61u);
     if (!DEC && valid && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
@@ -1608,7 +1627,7 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
         else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
         status_out[i] = status;
-        flags_out[i] = status == 0 ? (uint8_t) (fl | zmtp_msg_bits(ctl.zflags, i)) : 0;
+        flags_out[i] = status == 0 ? (uint8_t) (fl | frame_zbits<DEC>(big, i)) : 0;
         if (status != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this lane's plaintext stores first
             zero_bytes(dst, S - 33u);

@@ -541,6 +541,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         big(i, list_ctr, nbase);
     }
     call_state_end<DEC>(zs, ctl, cs, n);
+    frame_result_copy<DEC>(big);
     SEQ_STAMP(61u);
     if (!DEC && valid && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         else if ((tag[0] ^ wtag[0]) | (tag[1] ^ wtag[1]) | (tag[2] ^ wtag[2]) | (tag[3] ^ wtag[3]))
             status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
         status_out[i] = status;
-        flags_out[i] = status == 0 ? (uint8_t) (fl | zmtp_msg_bits(ctl.zflags, i)) : 0;
+        flags_out[i] = status == 0 ? (uint8_t) (fl | frame_zbits<DEC>(big, i)) : 0;
         if (status != 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the wave's stores of this frame first
             zero_bytes(dst, S - 33u);

@@ -290,13 +290,13 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
 // counts, off_wg[nwg] = m), and the links (round 4: in this kernel, no launch
 // of their own): candidate k is unlinked when its frame does not end at
 // candidate k+1 (the last one never does).  k+1 is the next entry of the same
-// list, or the first entry of the next non-empty list (nxt, from
-// k_zmtp_exsum), so no other workgroup's output is needed.  Per list: nb[k] =
+// list, or the first entry of the next non-empty list (found from the
+// counts), so no other workgroup's output of this launch is needed.  Per list: nb[k] =
 // the first unlinked index >= k in k's list (or none), first_w[w] = the first
 // unlinked index of list w (or none), wid[k] = w.
 __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint8_t *b, uint64_t n, const uint64_t *cand_wg,
                                                                const uint64_t *count_wg, const uint64_t *off_wg,
-                                                               const uint32_t *nxt, uint32_t nwg, uint64_t *cand,
+                                                               uint32_t nwg, uint64_t *cand,
                                                                uint64_t *nb, uint64_t *first_w, uint32_t *wid)
 {
     __shared__ unsigned long long sh[kZmtpThreads / 64];
@@ -304,6 +304,25 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint8_t *b,
     const uint32_t lane = tid & 63u, wv = tid >> 6;
     const uint64_t o = off_wg[w];
     const uint64_t *const list = cand_wg + (size_t) w * kZmtpWgCap;
+    // the first entry of the next non-empty list: the workgroup looks at the
+    // next 256 lists' counts at once (further only behind a 4 MiB gap)
+    __shared__ uint32_t sh_nx[kZmtpThreads / 64];
+    uint64_t after = kZmtpNone;
+    for (uint32_t w0 = w + 1; c > 0 && w0 < nwg; w0 += kZmtpThreads) {
+        const uint32_t q = w0 + tid;
+        const unsigned long long nz = __ballot(q < nwg && count_wg[q] != 0);
+        __syncthreads();
+        if (lane == 0)
+            sh_nx[wv] = nz ? w0 + 64u * wv + (uint32_t) __builtin_ctzll(nz) : nwg;
+        __syncthreads();
+        uint32_t f = nwg;
+        for (uint32_t k = 0; k < kZmtpThreads / 64; ++k)
+            f = sh_nx[k] < f ? sh_nx[k] : f;
+        if (f < nwg) {
+            after = cand_wg[(size_t) f * kZmtpWgCap];
+            break;
+        }
+    }
     unsigned long long carry = kZmtpNone; // the minimum over the later chunks
     for (int j = (int) ((c + kZmtpThreads - 1) / kZmtpThreads) - 1; j >= 0; --j) {
         const uint32_t k = (uint32_t) j * kZmtpThreads + tid;
@@ -312,11 +331,7 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint8_t *b,
             const uint64_t p = list[k];
             cand[o + k] = p;
             wid[o + k] = w;
-            uint64_t next = kZmtpNone;
-            if (k + 1 < c)
-                next = list[k + 1];
-            else if (nxt[w] < nwg)
-                next = cand_wg[(size_t) nxt[w] * kZmtpWgCap];
+            const uint64_t next = k + 1 < c ? list[k + 1] : after;
             uint32_t hdr;
             uint64_t size;
             zmtp_header(b, n, p, hdr, size);
@@ -355,94 +370,71 @@ constexpr uint32_t kZmtpNextThreads = 1024;
 template <uint32_t T>
 __device__ void zmtp_suffix_min(uint64_t *first_w, uint64_t count)
 {
-    __shared__ unsigned long long sh[T];
+    // (wave shuffles, one LDS exchange between the waves)
+    __shared__ unsigned long long sh[T / 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t per = (count + T - 1) / T;
     const uint64_t r0 = threadIdx.x * per < count ? threadIdx.x * per : count;
     const uint64_t r1 = r0 + per < count ? r0 + per : count;
-    unsigned long long mn = kZmtpNone;
+    unsigned long long x = kZmtpNone;
     for (uint64_t s = r0; s < r1; ++s)
-        mn = first_w[s] < mn ? first_w[s] : mn;
-    sh[threadIdx.x] = mn;
-    __syncthreads();
-    for (uint32_t d = 1; d < T; d <<= 1) {
-        const unsigned long long o = threadIdx.x + d < T ? sh[threadIdx.x + d] : kZmtpNone;
-        __syncthreads();
-        if (o < sh[threadIdx.x])
-            sh[threadIdx.x] = o;
-        __syncthreads();
+        x = first_w[s] < x ? first_w[s] : x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_down(x, d);
+        if (lane + d < 64u && y < x)
+            x = y;
     }
-    unsigned long long c = threadIdx.x + 1 < T ? sh[threadIdx.x + 1] : kZmtpNone;
+    if (lane == 0)
+        sh[wv] = x;
+    __syncthreads();
+    unsigned long long later = kZmtpNone; // the later waves' minimum
+    for (uint32_t q = wv + 1; q < T / 64; ++q)
+        later = sh[q] < later ? sh[q] : later;
+    const unsigned long long nx = __shfl_down(x, 1);
+    unsigned long long c = lane < 63u ? (nx < later ? nx : later) : later; // minimum over the later threads
     for (uint64_t s = r1; s-- > r0;) {
-        const unsigned long long x = first_w[s];
-        c = x < c ? x : c;
+        const unsigned long long v = first_w[s];
+        c = v < c ? v : c;
         first_w[s] = c;
     }
 }
 
 // Exclusive sum of v[0..n) into o[0..n] (o[n] = total) by one workgroup of
 // 1024 threads, each a contiguous run: the workgroups' candidate counts.
-// With nxt: nxt[i] = the first j > i with v[j] > 0, or n (the next non-empty
-// list, for k_zmtp_compact's links).
 constexpr uint32_t kZmtpScan1 = 1024;
-__device__ void zmtp_next_nonempty(const uint64_t *v, uint64_t n, uint32_t *nxt)
+__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_exsum(const uint64_t *v, uint64_t n, uint64_t *o)
 {
-    __shared__ unsigned long long sh[kZmtpScan1];
-    const uint64_t per = (n + kZmtpScan1 - 1) / kZmtpScan1;
-    const uint64_t r0 = threadIdx.x * per < n ? threadIdx.x * per : n, r1 = r0 + per < n ? r0 + per : n;
-    unsigned long long mn = n;
-    for (uint64_t i = r1; i-- > r0;)
-        mn = v[i] ? i : mn;
-    sh[threadIdx.x] = mn;
-    __syncthreads();
-    for (uint32_t d = 1; d < kZmtpScan1; d <<= 1) {
-        const unsigned long long o = threadIdx.x + d < kZmtpScan1 ? sh[threadIdx.x + d] : n;
-        __syncthreads();
-        if (o < sh[threadIdx.x])
-            sh[threadIdx.x] = o;
-        __syncthreads();
-    }
-    unsigned long long c = threadIdx.x + 1 < kZmtpScan1 ? sh[threadIdx.x + 1] : n;
-    for (uint64_t i = r1; i-- > r0;) {
-        nxt[i] = (uint32_t) c;
-        if (v[i])
-            c = i;
-    }
-}
-
-__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_exsum(const uint64_t *v, uint64_t n, uint64_t *o, uint32_t *nxt)
-{
-    __shared__ unsigned long long sh[kZmtpScan1];
+    // (wave shuffles, one LDS exchange between the waves)
+    __shared__ unsigned long long sh[kZmtpScan1 / 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t per = (n + kZmtpScan1 - 1) / kZmtpScan1;
     const uint64_t r0 = threadIdx.x * per < n ? threadIdx.x * per : n, r1 = r0 + per < n ? r0 + per : n;
     unsigned long long t = 0;
     for (uint64_t i = r0; i < r1; ++i)
         t += v[i];
-    sh[threadIdx.x] = t;
+    unsigned long long x = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_up(x, d);
+        if ((int) lane >= d)
+            x += y;
+    }
+    if (lane == 63)
+        sh[wv] = x;
     __syncthreads();
-    for (uint32_t d = 1; d < kZmtpScan1; d <<= 1) {
-        const unsigned long long x = threadIdx.x >= d ? sh[threadIdx.x - d] : 0ull;
-        __syncthreads();
-        sh[threadIdx.x] += x;
-        __syncthreads();
+    unsigned long long acc = x - t, tot = 0;
+    for (uint32_t q = 0; q < kZmtpScan1 / 64; ++q) {
+        acc += q < wv ? sh[q] : 0ull;
+        tot += sh[q];
     }
-    unsigned long long acc = sh[threadIdx.x] - t;
     for (uint64_t i = r0; i < r1; ++i) {
-        const unsigned long long x = v[i];
+        const unsigned long long y = v[i];
         o[i] = acc;
-        acc += x;
+        acc += y;
     }
-    if (threadIdx.x == kZmtpScan1 - 1)
-        o[n] = sh[kZmtpScan1 - 1];
-    if (nxt) {
-        __syncthreads();
-        zmtp_next_nonempty(v, n, nxt);
-    }
-}
-
-// nxt alone (streams whose counts hipCUB scans)
-__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_nxt(const uint64_t *v, uint64_t n, uint32_t *nxt)
-{
-    zmtp_next_nonempty(v, n, nxt);
+    if (threadIdx.x == 0)
+        o[n] = tot;
 }
 
 // Parse state written by k_zmtp_walk (device).  It begins with the call's

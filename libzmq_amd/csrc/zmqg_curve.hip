@@ -173,7 +173,6 @@ struct ZmtpWs {
     uint64_t *cand = nullptr;             // [c_cap] sorted candidates
     uint64_t *nb = nullptr;               // [c_cap] next unlinked candidate in the 256-candidate segment
     uint64_t *first_w = nullptr;          // [g_cap + 1] first unlinked candidate in workgroup lists >= w
-    uint32_t *nxt = nullptr;              // [g_cap + 1] next non-empty workgroup list
     uint32_t *wid = nullptr;              // [c_cap] each candidate's workgroup list
     uint64_t *run = nullptr;              // [2 (f_cap + 1)]
     uint64_t *runpre = nullptr;           // [f_cap + 1]
@@ -618,6 +617,9 @@ struct DecodeHead {
     const DevSession *sessions;
     uint32_t max_sessions;
     BigRecords R;
+    const uint8_t *zflags = nullptr;             // zmqg_decode_zmtp (frame_zbits)
+    const unsigned long long *res_src = nullptr; // zmqg_decode_zmtp (frame_result_copy)
+    unsigned long long *res_dst = nullptr;
     __device__ void operator()(uint32_t i, unsigned long long *list_ctr, uint64_t nbase) const;
 };
 
@@ -2339,7 +2341,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
             (void) hipFree(p);
     {
         ZmtpWs &z = ctx->zw;
-        void *zp[] = {z.F,      z.wire_off, z.cand_wg, z.count_wg, z.off_wg, z.cand, z.nb,   z.first_w, z.nxt,
+        void *zp[] = {z.F,      z.wire_off, z.cand_wg, z.count_wg, z.off_wg, z.cand, z.nb,   z.first_w,
                       z.wid,    z.run,      z.runpre,  z.sid_fill, z.fflags, z.walk, z.res,  z.temp};
         for (void *p : zp)
             if (p)
@@ -2732,9 +2734,6 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     const bool multi = ctx->sort_bits > 0;
     FrameCtl ctl{};
     ctl.post = w.post;
-    ctl.zflags = zflags;
-    ctl.res_src = (const unsigned long long *) zwalk;
-    ctl.res_dst = (unsigned long long *) zres;
     unsigned long long *smax = nullptr;
     if (opts) {
         ctl.max_len = opts->max_len;
@@ -2771,7 +2770,8 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     ProfSpan main(ctx, ZMQG_PROF_DECODE_MAIN, st);
     launch_frames<true>(G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out, ctx->sessions,
                         ctx->max_sessions, flags_out, status_out, rp,
-                        DecodeHead{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R},
+                        DecodeHead{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R,
+                                   zflags, (const unsigned long long *) zwalk, (unsigned long long *) zres},
                         w.zs, ctl);
     ZCHECK(ctx, hipGetLastError());
     main.end();
@@ -3200,8 +3200,7 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         while (cap < nwg)
             cap *= 2;
         if ((rc = grow(ctx, z.cand_wg, cap * kZmtpWgCap, st)) || (rc = grow(ctx, z.count_wg, cap + 1, st)) ||
-            (rc = grow(ctx, z.off_wg, cap + 1, st)) || (rc = grow(ctx, z.first_w, cap + 1, st)) ||
-            (rc = grow(ctx, z.nxt, cap + 1, st)))
+            (rc = grow(ctx, z.off_wg, cap + 1, st)) || (rc = grow(ctx, z.first_w, cap + 1, st)))
             return rc;
         z.g_cap = cap;
     }
@@ -3232,15 +3231,14 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
     const uint32_t pg = (uint32_t) (ctx->cus > 0 ? 4 * ctx->cus : 1024);
     const uint64_t *m_p = z.off_wg + nwg; // the candidate count, on the device
     // 1. candidates, in stream order: per-workgroup lists, their counts'
-    // exclusive sum (and each list's next non-empty one), the lists
-    // concatenated with their links
+    // exclusive sum, the lists concatenated with their links
     hipLaunchKernelGGL(k_zmtp_scan, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
                        z.count_wg);
     ZCHECK(ctx, hipGetLastError());
     // (ZMQG_ZMTP_CUB: the large-stream form at any size, for its tests)
     if (nwg <= 8u * kZmtpScan1 && !getenv("ZMQG_ZMTP_CUB")) {
         hipLaunchKernelGGL(k_zmtp_exsum, dim3(1), dim3(kZmtpScan1), 0, st, (const uint64_t *) z.count_wg, nwg,
-                           z.off_wg, z.nxt);
+                           z.off_wg);
         ZCHECK(ctx, hipGetLastError());
     } else {
         size_t need = 0;
@@ -3250,11 +3248,9 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         ZCHECK(ctx, hipMemsetAsync(z.count_wg + nwg, 0, sizeof(uint64_t), st));
         size_t tb = z.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.count_wg, z.off_wg, (int) (nwg + 1), st));
-        hipLaunchKernelGGL(k_zmtp_nxt, dim3(1), dim3(kZmtpScan1), 0, st, (const uint64_t *) z.count_wg, nwg, z.nxt);
-        ZCHECK(ctx, hipGetLastError());
     }
     hipLaunchKernelGGL(k_zmtp_compact, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand_wg,
-                       (const uint64_t *) z.count_wg, (const uint64_t *) z.off_wg, (const uint32_t *) z.nxt, g, z.cand,
+                       (const uint64_t *) z.count_wg, (const uint64_t *) z.off_wg, g, z.cand,
                        z.nb, z.first_w, z.wid);
     ZCHECK(ctx, hipGetLastError());
     // 2. the first unlinked candidate after each list, then the walk (one launch)
