@@ -130,3 +130,52 @@ def test_without_carry_the_fold_wraps():
         except Wrap:
             wrapped += 1
     assert wrapped > 0
+
+
+def prefix_poly(blocks, r):
+    """H = sum m_k r^(N-k) as k_msg computes it since round 4 (before + s):
+    c = ceil(N/64) blocks per lane (Horner), nl = ceil(N/c) lanes
+    right-aligned (zero blocks in front), each lane's Horner value times its
+    power P_v = (r^c)^(nl-1-v) from a suffix-product scan over the lanes
+    (log2 levels of one multiply), then a carried sum over the lanes."""
+    n = len(blocks)
+    rf = to_fe(r)
+    c = (n + 63) // 64
+    nl = (n + c - 1) // c
+    pad = c * nl - n
+    hs = []
+    for v in range(64):
+        h = [0] * 5
+        if v < nl:
+            for t in range(c):
+                k = c * v + t - pad
+                if k >= 0:
+                    m = to_fe(blocks[k] & ((1 << 128) - 1))
+                    m[4] += blocks[k] >> 128 << 24
+                    h = fe_mul([h[i] + m[i] for i in range(5)], rf)
+        hs.append(h)
+    r2 = fe_mul(rf, rf)
+    x = [rf, r2, fe_mul(r2, rf), fe_mul(r2, r2)][c - 1]
+    one = [1, 0, 0, 0, 0]
+    pw = [x if v < nl - 1 else one for v in range(64)]
+    s = 0
+    while (1 << s) < nl:
+        pw = [fe_mul(pw[v], pw[v + (1 << s)]) if v + (1 << s) < nl else pw[v] for v in range(64)]
+        s += 1
+    terms = [fe_mul(hs[v], pw[v]) if v < nl else [0] * 5 for v in range(64)]
+    d = 1
+    while d < 64:  # the shuffle levels of the sum, each carried
+        terms = [fe_carry([terms[v][i] + (terms[v + d][i] if v + d < 64 else 0) for i in range(5)])
+                 for v in range(64)]
+        d <<= 1
+    return from_fe(terms[0]) % P
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_prefix_equals_horner(seed):
+    rnd = random.Random(100 + seed)
+    for _ in range(150):
+        r = rnd.getrandbits(128) & 0x0ffffffc0ffffffc0ffffffc0fffffff
+        n = rnd.choice([1, 2, 3, 4, 5, 63, 64, 65, 66, 128, 129, 130, 192, 193, 200, 249, 252, 253, 254])
+        blocks = [rnd.getrandbits(128) | (1 << 128) for _ in range(n)]
+        assert prefix_poly(blocks, r) == horner(blocks, r)
