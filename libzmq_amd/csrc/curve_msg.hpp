@@ -54,31 +54,34 @@ struct MsgArgs {
 // flight at once -- up to four dwordx4 per lane, 4 KiB per wave -- before any
 // of them is used; other alignments take the general byte/word form.
 typedef u32x4 msg_u32x4_u1 __attribute__((aligned(1)));
-__device__ __forceinline__ void msg_load_lds(uint8_t *lds, const uint8_t *g, uint32_t n, uint32_t lane)
+constexpr uint32_t kMsgThreads = 256; // four waves: one Salsa20 block per quad of lanes (salsa20_quad)
+
+__device__ __forceinline__ void msg_load_lds(uint8_t *lds, const uint8_t *g, uint32_t n, uint32_t tid)
 {
+    constexpr uint32_t T = kMsgThreads;
     if (((uintptr_t) g & 15u) == 0 && n <= kMsgMaxStream) {
         const uint32_t ng = n >> 4, tail = n & 15u;
-        u32x4 v[kMsgMaxStream / 16 / 64];
+        u32x4 v[kMsgMaxStream / 16 / T];
 #pragma unroll
-        for (uint32_t j = 0; j < kMsgMaxStream / 16 / 64; ++j)
-            if (lane + 64u * j < ng)
-                v[j] = *(const GCU4 *) (uintptr_t) (g + 16u * (lane + 64u * j));
-        const uint8_t tb = lane < tail ? g[16u * ng + lane] : 0;
+        for (uint32_t j = 0; j < kMsgMaxStream / 16 / T; ++j)
+            if (tid + T * j < ng)
+                v[j] = *(const GCU4 *) (uintptr_t) (g + 16u * (tid + T * j));
+        const uint8_t tb = tid < tail ? g[16u * ng + tid] : 0;
 #pragma unroll
-        for (uint32_t j = 0; j < kMsgMaxStream / 16 / 64; ++j)
-            if (lane + 64u * j < ng)
-                *(msg_u32x4_u1 *) (lds + 16u * (lane + 64u * j)) = v[j];
-        if (lane < tail)
-            lds[16u * ng + lane] = tb;
+        for (uint32_t j = 0; j < kMsgMaxStream / 16 / T; ++j)
+            if (tid + T * j < ng)
+                *(msg_u32x4_u1 *) (lds + 16u * (tid + T * j)) = v[j];
+        if (tid < tail)
+            lds[16u * ng + tid] = tb;
         return;
     }
     const uint32_t head = (4u - ((uint32_t) (uintptr_t) g & 3u)) & 3u;
     const uint32_t h = head < n ? head : n;
-    for (uint32_t k = lane; k < h; k += 64)
+    for (uint32_t k = tid; k < h; k += T)
         lds[k] = g[k];
     const uint32_t nw = (n - h) >> 2;
     const uint32_t *gw = (const uint32_t *) (uintptr_t) (g + h);
-    for (uint32_t k = lane; k < nw; k += 64) {
+    for (uint32_t k = tid; k < nw; k += T) {
         const uint32_t v = gw[k];
         uint8_t *p = lds + h + 4 * k;
         p[0] = (uint8_t) v;
@@ -86,29 +89,30 @@ __device__ __forceinline__ void msg_load_lds(uint8_t *lds, const uint8_t *g, uin
         p[2] = (uint8_t) (v >> 16);
         p[3] = (uint8_t) (v >> 24);
     }
-    for (uint32_t k = h + 4 * nw + lane; k < n; k += 64)
+    for (uint32_t k = h + 4 * nw + tid; k < n; k += T)
         lds[k] = g[k];
 }
 
-__device__ __forceinline__ void msg_store_g(uint8_t *g, const uint8_t *lds, uint32_t n, uint32_t lane)
+__device__ __forceinline__ void msg_store_g(uint8_t *g, const uint8_t *lds, uint32_t n, uint32_t tid)
 {
+    constexpr uint32_t T = kMsgThreads;
     const uint32_t head = (4u - ((uint32_t) (uintptr_t) g & 3u)) & 3u;
     const uint32_t h = head < n ? head : n;
-    for (uint32_t k = lane; k < h; k += 64)
+    for (uint32_t k = tid; k < h; k += T)
         g[k] = lds[k];
     const uint32_t nw = (n - h) >> 2;
     uint32_t *gw = (uint32_t *) (uintptr_t) (g + h);
-    for (uint32_t k = lane; k < nw; k += 64) {
+    for (uint32_t k = tid; k < nw; k += T) {
         const uint8_t *p = lds + h + 4 * k;
         gw[k] = (uint32_t) p[0] | ((uint32_t) p[1] << 8) | ((uint32_t) p[2] << 16) | ((uint32_t) p[3] << 24);
     }
-    for (uint32_t k = h + 4 * nw + lane; k < n; k += 64)
+    for (uint32_t k = h + 4 * nw + tid; k < n; k += T)
         g[k] = lds[k];
 }
 
-__device__ __forceinline__ void msg_zero_g(uint8_t *g, uint32_t n, uint32_t lane)
+__device__ __forceinline__ void msg_zero_g(uint8_t *g, uint32_t n, uint32_t tid)
 {
-    for (uint32_t k = lane; k < n; k += 64)
+    for (uint32_t k = tid; k < n; k += kMsgThreads)
         g[k] = 0;
 }
 
@@ -175,28 +179,34 @@ __device__ __forceinline__ void msg_done(uint32_t *done)
         __hip_atomic_store(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// salsa20_block with the double rounds in a loop: a single launch executes
-// it once per lane, so a tenth of the code (fewer instruction-cache misses
-// on a cold CU) costs only the loop's scalar branch.
-__device__ __forceinline__ void salsa20_block_rolled(uint32_t out[16], const uint32_t k[8], uint32_t n0, uint32_t n1,
-                                                     uint32_t ctr)
+// One Salsa20 block on a quad of lanes (round 4): lane q of the quad holds
+// column q's quarter-round (a, b, c, d) = x[5q], x[5q+4], x[5q+8], x[5q+12]
+// (indices mod 16), so a column round is one quarter-round per lane.  Row q's
+// quarter-round (x[5q], x[5q+1], x[5q+2], x[5q+3], within row q) finds its b,
+// c, d in lanes q+1, q+2, q+3 of the quad, as their d, c, b: three quad
+// permutations (DPP quad_perm) before the row round and their inverses after.
+// A block costs a lane 240 VALU operations instead of 960, so the keystream
+// of a one-message launch takes a quarter of the time (the launch spends four
+// waves instead of one).
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v)
 {
-    uint32_t x[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, ctr, 0, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+    return (uint32_t) __builtin_amdgcn_mov_dpp((int) v, CTRL, 0xf, 0xf, false);
+}
+constexpr int kQuadNext = 0x39, kQuadHalf = 0x4e, kQuadPrev = 0x93; // lane q reads q+1 / q+2 / q+3 (mod 4)
+
+__device__ __forceinline__ void salsa20_quad(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d)
+{
+    // (a rolled loop: one launch runs it once, from a cold instruction cache)
 #pragma unroll 1
-    for (int rr = 0; rr < 10; ++rr) {
-        ZMQG_QR(x[0], x[4], x[8], x[12]);
-        ZMQG_QR(x[5], x[9], x[13], x[1]);
-        ZMQG_QR(x[10], x[14], x[2], x[6]);
-        ZMQG_QR(x[15], x[3], x[7], x[11]);
-        ZMQG_QR(x[0], x[1], x[2], x[3]);
-        ZMQG_QR(x[5], x[6], x[7], x[4]);
-        ZMQG_QR(x[10], x[11], x[8], x[9]);
-        ZMQG_QR(x[15], x[12], x[13], x[14]);
+    for (int r = 0; r < 10; ++r) {
+        ZMQG_QR(a, b, c, d); // column round
+        uint32_t B = quad_perm<kQuadNext>(d), C = quad_perm<kQuadHalf>(c), D = quad_perm<kQuadPrev>(b);
+        ZMQG_QR(a, B, C, D); // row round
+        d = quad_perm<kQuadPrev>(B);
+        c = quad_perm<kQuadHalf>(C);
+        b = quad_perm<kQuadNext>(D);
     }
-    const uint32_t in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, ctr, 0, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        out[i] = x[i] + in[i];
 }
 
 // The message itself as a kernel argument (CAP bytes, zero-padded to a
@@ -212,31 +222,31 @@ constexpr uint32_t kMsgInlineMax = 3968; // kernel arguments are limited to 4 Ki
 // LDS <- the inline message (n bytes) at byte offset lds (any alignment)
 typedef uint32_t msg_u32_u1 __attribute__((aligned(1)));
 template <uint32_t CAP>
-__device__ __forceinline__ void msg_inline_lds(uint8_t *lds, const MsgInline<CAP> &d, uint32_t n, uint32_t lane)
+__device__ __forceinline__ void msg_inline_lds(uint8_t *lds, const MsgInline<CAP> &d, uint32_t n, uint32_t tid)
 {
     const uint32_t nw = (n + 3) >> 2;
 #pragma unroll
-    for (uint32_t j = 0; j < (CAP / 4 + 63) / 64; ++j) {
-        const uint32_t i = lane + 64u * j;
+    for (uint32_t j = 0; j < (CAP / 4 + kMsgThreads - 1) / kMsgThreads; ++j) {
+        const uint32_t i = tid + kMsgThreads * j;
         if (i < nw)
             *(msg_u32_u1 *) (lds + 4u * i) = d.w[i];
     }
 }
 
 template <bool DEC, uint32_t CAP>
-__global__ __launch_bounds__(64) void k_msg(MsgArgs a, MsgInline<CAP> d)
+__global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d)
 {
     __shared__ uint32_t st_w[kMsgMaxStream / 4 + 16]; // the stream image: 32 bytes, then the message bytes
+    __shared__ int32_t sh_status;
     uint8_t *const st = (uint8_t *) st_w;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const bool sid_ok = a.sid < a.max_sessions;
     const DevSession &ses = a.sessions[sid_ok ? a.sid : 0u];
     uint32_t key[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t)
         key[t] = DEC ? ses.dec_key[t] : ses.enc_key[t];
-    // decode: the peer nonce is read now, beside the message's PCIe round
-    // trip, not after it
+    // decode: the peer nonce is read now, beside the key's round trip
     const unsigned long long peer = DEC && sid_ok ? a.peer[a.sid] : 0ull;
 
     // ---- 1. the message into LDS at its stream position; header checks
@@ -248,14 +258,14 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a, MsgInline<CAP> d)
         uint32_t hw[3];
         const uint32_t hl = plaintext_header(a.flags, ses.downgrade_sub, hw);
         m = hl + a.len;
-        if (lane < 8)
-            st_w[lane] = 0;
-        if (lane < hl)
-            st[32 + lane] = (uint8_t) (hw[lane >> 2] >> (8 * (lane & 3)));
+        if (tid < 8)
+            st_w[tid] = 0;
+        if (tid < hl)
+            st[32 + tid] = (uint8_t) (hw[tid >> 2] >> (8 * (tid & 3)));
         if (CAP)
-            msg_inline_lds(st + 32 + hl, d, a.len, lane);
+            msg_inline_lds(st + 32 + hl, d, a.len, tid);
         else if (!(ZMQG_MSG_ABLATE & 32))
-            msg_load_lds(st + 32 + hl, a.in, a.len, lane);
+            msg_load_lds(st + 32 + hl, a.in, a.len, tid);
         nc = a.nonce;
         n0 = bswap32((uint32_t) (nc >> 32));
         n1 = bswap32((uint32_t) nc);
@@ -264,9 +274,9 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a, MsgInline<CAP> d)
     } else {
         const uint32_t L = a.len;
         if (CAP)
-            msg_inline_lds(st, d, L, lane);
+            msg_inline_lds(st, d, L, tid);
         else if (!(ZMQG_MSG_ABLATE & 32))
-            msg_load_lds(st, a.in, L, lane);
+            msg_load_lds(st, a.in, L, tid);
         __syncthreads();
         // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
         const uint32_t b0 = L ? st[0] : 0u;
@@ -293,106 +303,138 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a, MsgInline<CAP> d)
     // zero the bytes after the message up to the next 16-byte block (Poly1305
     // pads a partial last block with zeros)
     const uint32_t end = 32 + m;
-    if (lane < 16 && end + lane < kMsgMaxStream + 64)
-        st[end + lane] = 0;
+    if (tid < 16 && end + tid < kMsgMaxStream + 64)
+        st[end + tid] = 0;
     __syncthreads();
-    if (DEC && status == 0 && lane == 0)
+    if (DEC && status == 0 && tid == 0)
         a.peer[a.sid] = nc;
 
-    // ---- 2. keystream block `lane`, XOR of its window
-    const uint32_t nb = (end + 63) >> 6;
-    uint32_t ks[16];
+    // ---- 2. keystream block blk on its quad of lanes, XOR of its window's
+    // four words of the quad's lane
+    const uint32_t nb = (end + 63) >> 6, blk = tid >> 2, q = tid & 3u;
+    // (a, b, c, d) = x[5q], x[5q+4], x[5q+8], x[5q+12] of block blk
+    const uint32_t sig = q == 0 ? SIGMA0 : q == 1 ? SIGMA1 : q == 2 ? SIGMA2 : SIGMA3;
+    const uint32_t ib = q == 0 ? key[3] : q == 1 ? 0u : q == 2 ? key[7] : key[2];
+    const uint32_t ic = q == 0 ? blk : q == 1 ? key[6] : q == 2 ? key[1] : n1;
+    const uint32_t id = q == 0 ? key[5] : q == 1 ? key[0] : q == 2 ? n0 : key[4];
+    uint32_t ka = sig, kb = ib, kc = ic, kd = id;
     if (ZMQG_MSG_ABLATE & 4) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            ks[k] = key[k & 7] ^ (lane * 0x9e3779b9u + k);
+        ka ^= blk * 0x9e3779b9u;
+        kc ^= kb;
     } else {
-        salsa20_block_rolled(ks, key, n0, n1, lane);
+        salsa20_quad(ka, kb, kc, kd);
     }
-    uint32_t w[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        w[k] = st_w[16 * lane + k];
-    // the Poly1305 key: keystream bytes 0..31 of block 0
+    ka += sig;
+    kb += ib;
+    kc += ic;
+    kd += id;
+    // the Poly1305 key: keystream words 0..7 of block 0 (lanes 0-3: words 0
+    // 4 8 12 / 5 9 13 1 / 10 14 2 6 / 15 3 7 11; meaningful in wave 0 only)
     uint32_t pk[8];
+    pk[0] = __builtin_amdgcn_readlane(ka, 0);
+    pk[1] = __builtin_amdgcn_readlane(kd, 1);
+    pk[2] = __builtin_amdgcn_readlane(kc, 2);
+    pk[3] = __builtin_amdgcn_readlane(kb, 3);
+    pk[4] = __builtin_amdgcn_readlane(kb, 0);
+    pk[5] = __builtin_amdgcn_readlane(ka, 1);
+    pk[6] = __builtin_amdgcn_readlane(kd, 2);
+    pk[7] = __builtin_amdgcn_readlane(kc, 3);
+    const uint32_t ia = (5u * q) & 15u; // word index of register a; b, c, d follow at +4, +8, +12 (mod 16)
+    uint32_t o[4];                      // this lane's output words (ciphertext or plaintext) of block blk
+    {
+        const uint32_t ks[4] = {ka, kb, kc, kd};
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        pk[k] = __builtin_amdgcn_readfirstlane(ks[k]);
-    uint32_t o[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        o[k] = (lane == 0 && k < 8) ? 0u : w[k] ^ ks[k];
-    // bytes past the message stay zero in the image (the Poly1305 padding)
-    if (lane < nb) {
-        const int nv = (int) end - 64 * (int) lane;
-        if (nv < 64)
-            mask_tail(o, nv);
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t wi = (ia + 4u * k) & 15u;
+            const int nv = (int) end - (int) (64u * blk + 4u * wi); // valid bytes of this word
+            const uint32_t mk = nv >= 4 ? 0xffffffffu : (nv <= 0 ? 0u : ((1u << (8 * nv)) - 1u));
+            const uint32_t x = blk < nb ? st_w[16u * blk + wi] : 0u;
+            o[k] = (blk == 0 && wi < 8) ? 0u : ((x ^ ks[k]) & mk);
+        }
     }
     if (!DEC) { // the ciphertext image replaces the plaintext
         __syncthreads();
-        if (lane < nb)
+        if (blk < nb)
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                st_w[16 * lane + k] = o[k];
+            for (int k = 0; k < 4; ++k)
+                st_w[16u * blk + ((ia + 4u * k) & 15u)] = o[k];
         __syncthreads();
     }
 
-    // ---- 3. Poly1305 over the ciphertext (stream bytes 32 .. 32+m)
-    const fe r = poly_r_from_key(pk[0], pk[1], pk[2], pk[3]);
-    // nl lanes of four blocks each, right-aligned in the smallest power-of-
-    // two span S that holds them (a short message needs few or no levels)
-    const uint32_t N = (m + 15) >> 4, nl = (N + 3) >> 2, pad = 4 * nl - N;
-    uint32_t levels = 0;
-    while ((1u << levels) < nl)
-        ++levels;
-    const uint32_t S = 1u << levels;
-    fe h = fe_zero();
-    const int seg = (int) lane - (int) (S - nl);
-    if (seg >= 0 && lane < S) {
-        const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+    // ---- 3. Poly1305 over the ciphertext (stream bytes 32 .. 32+m), wave 0:
+    // c = ceil(N/64) blocks per lane (a Horner sum), nl = ceil(N/c) lanes
+    // right-aligned (zero blocks in front of a Horner sum change nothing);
+    // lane v's sum is worth P_v = (r^c)^(nl-1-v), which a suffix-product scan
+    // over the lanes gives in log2(nl) levels of one multiply each; then the
+    // lanes' terms are summed (tests/test_poly_tree_model.py models it)
+    uint32_t tag[4] = {0, 0, 0, 0};
+    if (tid < 64) {
+        const fe r = poly_r_from_key(pk[0], pk[1], pk[2], pk[3]);
+        const uint32_t N = (m + 15) >> 4, c = N ? (N + 63) >> 6 : 1u, nl = (N + c - 1) / c, pad = c * nl - N;
+        uint32_t levels = 0;
+        while ((1u << levels) < nl)
+            ++levels;
+        fe h = fe_zero();
+        if (lane < nl) {
+            const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int k = 4 * seg + t - (int) pad;
-            if (k >= 0) {
-                const uint32_t *b = st_w + 8 + 4 * k;
-                uint32_t b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3], hib = 1u << 24;
-                const uint32_t rem = m - 16u * (uint32_t) k;
-                if (rem < 16u) { // partial last block: 0x01 after the data, no 2^128
-                    const uint32_t sh = 8u * (rem & 3u), wi = rem >> 2, one = 1u << sh;
-                    b0 |= wi == 0 ? one : 0u;
-                    b1 |= wi == 1 ? one : 0u;
-                    b2 |= wi == 2 ? one : 0u;
-                    b3 |= wi == 3 ? one : 0u;
-                    hib = 0;
+            for (uint32_t t = 0; t < 4; ++t) {
+                const int k = (int) (c * lane + t) - (int) pad;
+                if (t < c && k >= 0) {
+                    const uint32_t *bp = st_w + 8 + 4 * k;
+                    uint32_t b0 = bp[0], b1 = bp[1], b2 = bp[2], b3 = bp[3], hib = 1u << 24;
+                    const uint32_t rem = m - 16u * (uint32_t) k;
+                    if (rem < 16u) { // partial last block: 0x01 after the data, no 2^128
+                        const uint32_t sh = 8u * (rem & 3u), wi = rem >> 2, one = 1u << sh;
+                        b0 |= wi == 0 ? one : 0u;
+                        b1 |= wi == 1 ? one : 0u;
+                        b2 |= wi == 2 ? one : 0u;
+                        b3 |= wi == 3 ? one : 0u;
+                        hib = 0;
+                    }
+                    fe_add_block(h, b0, b1, b2, b3, hib);
+                    fe_mul_s(h, r, s1, s2, s3, s4);
                 }
-                fe_add_block(h, b0, b1, b2, b3, hib);
-                fe_mul_s(h, r, s1, s2, s3, s4);
             }
         }
-    }
-    if (levels && !(ZMQG_MSG_ABLATE & 8)) {
-        fe p = r;
-        fe_mul(p, r);
-        fe_mul(p, p); // r^4
-        // (a rolled loop: one launch runs this once, from a cold instruction cache)
+        if (levels && !(ZMQG_MSG_ABLATE & 8)) {
+            // x = r^c (c uniform, 1..4)
+            fe x = r;
+            if (c > 1) {
+                fe r2 = r;
+                fe_mul(r2, r);
+                x = r2;
+                if (c == 3)
+                    fe_mul(x, r);
+                else if (c == 4)
+                    fe_mul(x, r2);
+            }
+            fe pw = fe_zero();
+            pw.l[0] = 1;
+            if (lane + 1 < nl)
+                pw = x;
+            // (rolled loops: one launch runs them once, from a cold instruction cache)
 #pragma unroll 1
-        for (uint32_t s = 0; s < levels; ++s) {
-            const fe hn = fe_shfl_down(h, 1u << s);
-            if ((lane & ((2u << s) - 1u)) == 0) {
-                fe_mul(h, p);
-                fe_add(h, hn);
-                fe_carry(h); // (the next level multiplies it again)
+            for (uint32_t s = 0; s < levels; ++s) {
+                const fe o = fe_shfl_down(pw, 1u << s);
+                if (lane + (1u << s) < nl)
+                    fe_mul(pw, o);
             }
-            if (s + 1 < levels)
-                fe_mul(p, p);
+            fe_mul(h, pw);
+#pragma unroll 1
+            for (uint32_t s = 0; s < levels; ++s) {
+                const fe o = fe_shfl_down(h, 1u << s);
+                if (lane + (1u << s) < 64u)
+                    fe_add(h, o);
+                fe_carry(h);
+            }
         }
+        poly_finish(h, pk + 4, tag);
     }
-    uint32_t tag[4];
-    poly_finish(h, pk + 4, tag);
 
     // ---- 4. results
     if (!DEC) {
-        if (lane == 0) {
+        if (tid == 0) {
             st_w[0] = 0x53454d07u; // "\x07MES"
             st_w[1] = 0x45474153u; // "SAGE"
             st_w[2] = n0;
@@ -404,38 +446,40 @@ __global__ __launch_bounds__(64) void k_msg(MsgArgs a, MsgInline<CAP> d)
         __syncthreads();
         if (status == 0)
             if (!(ZMQG_MSG_ABLATE & 16))
-                msg_store_g(a.out, st, end, lane);
-        if (lane == 0 && a.status)
+                msg_store_g(a.out, st, end, tid);
+        if (tid == 0 && a.status)
             *a.status = status;
         msg_done(a.done);
         return;
     }
-    if (status == 0) {
-        const uint32_t t0 = __builtin_amdgcn_readfirstlane(tag[0]), t1 = __builtin_amdgcn_readfirstlane(tag[1]),
-                       t2 = __builtin_amdgcn_readfirstlane(tag[2]), t3 = __builtin_amdgcn_readfirstlane(tag[3]);
-        if ((t0 ^ st_w[4]) | (t1 ^ st_w[5]) | (t2 ^ st_w[6]) | (t3 ^ st_w[7]))
-            status = ZMQG_ERR_CRYPTOGRAPHIC;
+    if (tid == 0) {
+        if (status == 0) {
+            if ((tag[0] ^ st_w[4]) | (tag[1] ^ st_w[5]) | (tag[2] ^ st_w[6]) | (tag[3] ^ st_w[7]))
+                status = ZMQG_ERR_CRYPTOGRAPHIC;
+        }
+        sh_status = status;
     }
+    __syncthreads();
+    status = sh_status;
     const uint32_t P = a.len >= 33u ? a.len - 33u : 0u;
     if (status == 0) {
         // the plaintext image: flags byte at stream byte 32, payload after it
-        __syncthreads();
-        if (lane < nb)
+        if (blk < nb)
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                st_w[16 * lane + k] = o[k];
+            for (int k = 0; k < 4; ++k)
+                st_w[16u * blk + ((ia + 4u * k) & 15u)] = o[k];
         __syncthreads();
         if (!(ZMQG_MSG_ABLATE & 16))
-            msg_store_g(a.out, st + 33, P, lane);
-        if (lane == 0)
+            msg_store_g(a.out, st + 33, P, tid);
+        if (tid == 0)
             *a.flags_out = st[32] & 3u; // msg_t::more | msg_t::command (curve_mechanism_base.cpp:276)
     } else {
         if (!(ZMQG_MSG_ABLATE & 16))
-            msg_zero_g(a.out, P, lane);
-        if (lane == 0)
+            msg_zero_g(a.out, P, tid);
+        if (tid == 0)
             *a.flags_out = 0;
     }
-    if (lane == 0)
+    if (tid == 0)
         *a.status = status;
     msg_done(a.done);
 }

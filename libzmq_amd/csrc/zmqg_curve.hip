@@ -2248,7 +2248,7 @@ static void launch_msg(hipStream_t st, const MsgArgs &a, const uint8_t *msg, uin
         memset(inl.w, 0, sizeof inl.w);
         if (n)
             memcpy(inl.w, msg, n);
-        hipLaunchKernelGGL((k_msg<DEC, sizeof inl.w>), dim3(1), dim3(64), 0, st, a, inl);
+        hipLaunchKernelGGL((k_msg<DEC, sizeof inl.w>), dim3(1), dim3(kMsgThreads), 0, st, a, inl);
     };
     if (n <= 256u)
         go(MsgInline<256>{});
@@ -2257,7 +2257,7 @@ static void launch_msg(hipStream_t st, const MsgArgs &a, const uint8_t *msg, uin
     else if (n <= kMsgInlineMax)
         go(MsgInline<kMsgInlineMax>{});
     else
-        hipLaunchKernelGGL((k_msg<DEC, 0>), dim3(1), dim3(64), 0, st, a, MsgInline<0>{});
+        hipLaunchKernelGGL((k_msg<DEC, 0>), dim3(1), dim3(kMsgThreads), 0, st, a, MsgInline<0>{});
 }
 
 extern "C" {
