@@ -21,6 +21,7 @@ ap.add_argument("--size", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--sessions", type=int, default=1)
 ap.add_argument("--tag", default=os.environ.get("ZMQG_CURVE_LIB", "default"))
+ap.add_argument("--wire-align", type=int, default=1, help="wire frames at multiples of this many bytes")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 n, P = a.msgs, a.size
@@ -36,10 +37,11 @@ sid = t((np.arange(n) * a.sessions // n).astype(np.uint32), np.int32)
 flags = torch.zeros(n, dtype=torch.uint8, device=dev)
 in_off = t(np.arange(n, dtype=np.uint64) * P, np.int64)
 lens = t(np.full(n, P, np.uint32), np.int32)
-out_off = t(np.arange(n, dtype=np.uint64) * W, np.int64)
+WS = (W + a.wire_align - 1) // a.wire_align * a.wire_align  # wire stride
+out_off = t(np.arange(n, dtype=np.uint64) * WS, np.int64)
 wl = t(np.full(n, W, np.uint32), np.int32)
 nonce = t(np.arange(3, 3 + n, dtype=np.uint64), np.int64)
-wire = torch.zeros(n * W, dtype=torch.uint8, device=dev)
+wire = torch.zeros(n * WS, dtype=torch.uint8, device=dev)
 back = torch.zeros(n * P, dtype=torch.uint8, device=dev)
 fl = torch.zeros(n, dtype=torch.uint8, device=dev)
 st = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -61,7 +63,7 @@ for _ in range(a.iters):
     step()
 torch.cuda.synchronize()
 t1 = time.perf_counter()
-r = {"tag": a.tag, "msgs": n, "size": P, "step_us": (t1 - t0) / a.iters * 1e6}
+r = {"tag": a.tag, "wire_stride": WS, "msgs": n, "size": P, "step_us": (t1 - t0) / a.iters * 1e6}
 for name, ctx, k in [("enc_body_us", enc, 0), ("dec_body_us", dec, 1), ("enc_call_us", enc, 2),
                      ("dec_call_us", dec, 3), ("enc_kbody_us", enc, 4), ("dec_kbody_us", dec, 5)]:
     ms, cnt = ctx.get_profile(k)
