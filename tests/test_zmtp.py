@@ -122,17 +122,23 @@ def _stream_case(rng, case, precom, n=400):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["clean", "truncated", "planted", "flood", "large_small", "ping", "emsgsize",
-                                  "max_frames", "zmtp_flags", "sparse", "planted+cub", "sparse+cub"])
+                                  "max_frames", "zmtp_flags", "sparse", "planted+cub", "sparse+cub",
+                                  "zmtp_flags+g0", "zmtp_flags+g8", "ping+g0", "ping+g8"])
 def test_decode_zmtp_matches_oracle(torch_cuda, C, case, monkeypatch):
     """+cub: the candidate counts scanned by hipCUB (the form for streams above
-    128 MiB, ZMQG_ZMTP_CUB forces it) with the next-non-empty-list pass of its
-    own launch."""
+    128 MiB, ZMQG_ZMTP_CUB forces it).  +g0 / +g8: the decode's frame kernel
+    forced to the one-lane-per-frame forms (k_frames_seq / k_frames_lds;
+    these small streams otherwise take k_frames<4>), which OR the ZMTP flag
+    bits and copy the call's result themselves."""
     torch = torch_cuda
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     if case.endswith("+cub"):
         monkeypatch.setenv("ZMQG_ZMTP_CUB", "1")
         case = case[:-4]
+    elif case[-3:] in ("+g0", "+g8"):
+        monkeypatch.setenv("ZMQG_FRAMES_G", case[-1])
+        case = case[:-3]
     precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
     stream, max_msg, max_frames = _stream_case(rng, case, precom)
     ref = Z.parse(stream, max_msg, max_frames)
