@@ -121,3 +121,44 @@ def test_decode_msg_in_place(torch_cuda, C):
                                       st.ctypes.data_as(ctypes.c_void_p))
         assert rc == 0 and st[0] == 0 and fl[0] == 1
         assert w[:size].tobytes() == pay
+
+
+def test_msg_calls_follow_a_batch_on_another_stream(torch_cuda, C):
+    """A per-message call right after a batch call of the same ctx on another
+    stream, with no synchronisation between them: the message kernel runs on
+    the ctx's own stream after the batch (msg_order), so it sees the peer
+    nonce the batch advanced -- the next nonce decodes, an old one is a
+    replay (src/curve_mechanism_base.cpp:98-106)."""
+    torch = torch_cuda
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(21)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc, dec = _sessions(C, key)
+    n, P = 32768, 1024
+    W = C.wire_size(0, 0, P)
+    t = lambda a, d: torch.from_numpy(np.ascontiguousarray(a).view(d)).to(dev)
+    sid = torch.zeros(n, dtype=torch.int32, device=dev)
+    pay = torch.randint(0, 256, (n * P,), dtype=torch.uint8, device=dev)
+    in_off = t(np.arange(n, dtype=np.uint64) * P, np.int64)
+    lens = t(np.full(n, P, np.uint32), np.int32)
+    w_off = t(np.arange(n, dtype=np.uint64) * W, np.int64)
+    wl = t(np.full(n, W, np.uint32), np.int32)
+    wire = torch.zeros(n * W, dtype=torch.uint8, device=dev)
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    enc.encode_batch(sid, t(np.arange(3, 3 + n, dtype=np.uint64), np.int64), flags, in_off, lens, pay, w_off, wire)
+    torch.cuda.synchronize()
+    nxt = enc.encode_msg(0, 3 + n, 1, b"after the batch")
+    old = bytes(wire[5 * W:6 * W].cpu().numpy())
+    back = torch.zeros(n * P, dtype=torch.uint8, device=dev)
+    fl = torch.zeros(n, dtype=torch.uint8, device=dev)
+    st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        dec.decode_batch(sid, w_off, wl, wire, in_off, back, fl, st, stream=s.cuda_stream)
+    got, gfl, gst = dec.decode_msg(0, nxt)  # no synchronisation with s before this call
+    assert gst == 0 and got == b"after the batch" and gfl == 1
+    _, _, gst = dec.decode_msg(0, old)
+    assert gst == C.ERR_INVALID_SEQUENCE
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0 and torch.equal(back, pay)
+    assert dec.get_peer_nonce(0) == 3 + n
