@@ -155,7 +155,7 @@ __device__ __forceinline__ fe fe_shfl_down(const fe &x, uint32_t d)
 // scope: the results sit in mapped host memory), then lane 0 sets it.  The
 // host polls it instead of waiting for the stream (zmqg_*_msg).
 #ifndef ZMQG_MSG_ABLATE
-#define ZMQG_MSG_ABLATE 0 // (diagnostic builds only: 1 release-only fence, 2 no fence, 4 no Salsa20,
+#define ZMQG_MSG_ABLATE 0 // (diagnostic builds only: 1 full system fence, 2 no fence, 4 no Salsa20,
                           // 8 no Poly1305 tree, 16 no output stores, 32 no input loads)
 #endif
 __device__ __forceinline__ void msg_done(uint32_t *done)
@@ -166,14 +166,17 @@ __device__ __forceinline__ void msg_done(uint32_t *done)
             __hip_atomic_store(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
-    if (ZMQG_MSG_ABLATE & 1) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (ZMQG_MSG_ABLATE & 1) { // (the round-4 default before: a full system fence, acquire side included)
+        __threadfence_system();
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
-    __threadfence_system();
+    // every thread's writes released at system scope (the host reads them
+    // after seeing the word; nothing is read back here, so no acquire), then
+    // the word
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
