@@ -8,24 +8,25 @@
 // windows one after the other, and a workgroup takes part in the call-state
 // and look-back protocol.  For one message of at most kMsgMaxStream stream
 // bytes none of that is needed: the descriptors travel as kernel arguments,
-// the session key comes from HBM, and one wave spreads the message over its
-// lanes --
-//   1. the whole input (payload / wire frame) is loaded into LDS at its
-//      stream position (stream byte 32 + j = message byte j) by all lanes at
-//      once, so the only PCIe latency before the keystream is one round trip;
-//   2. lane b computes Salsa20 block b (stream bytes 64b .. 64b+63) and XORs
-//      its window;
-//   3. Poly1305 over the ciphertext in parallel: with N 16-byte blocks and
-//      nl = ceil(N/4) lanes holding 4 blocks each, the lanes are placed at the
-//      END of the wave (zero segments in front of a Horner sum change
-//      nothing), each lane's Horner value is worth r^(4*(63-lane)), and six
-//      shuffle levels combine h_v*r^(4*2^s) + h_(v+2^s);
-//   4. encode writes "\x07MESSAGE" || BE64(nonce) || tag || ciphertext;
-//      decode checks the header (src/mechanism_base.cpp:14-25,
-//      src/curve_mechanism_base.cpp:80-97), the replay rule (:98-106, the
-//      peer nonce advances before the MAC check) and the tag, and only then
-//      writes the payload (verified) or zeros (failed) -- libsodium's
-//      verify-then-decrypt order (:226-228).
+// the session key comes from HBM, and one workgroup of four waves spreads
+// the message over its lanes --
+//   1. the whole input (payload / wire frame) is laid out in LDS at its
+//      stream position (stream byte 32 + j = message byte j) from the kernel
+//      arguments (or, above kMsgInlineMax, from memory in one round trip);
+//   2. the quad of lanes 4b .. 4b+3 computes Salsa20 block b (stream bytes
+//      64b .. 64b+63, salsa20_quad) and each lane XORs its four words;
+//   3. Poly1305 over the ciphertext on wave 0: a Horner sum of c = ceil(N/64)
+//      blocks per lane, each lane's sum times its power of r^c from a DPP
+//      prefix product over the lanes, and a DPP row sum;
+//   4. meanwhile waves 1-3 store encode's "\x07MESSAGE" || BE64(nonce) ||
+//      ciphertext and wave 0 adds the tag; decode checks the header
+//      (src/mechanism_base.cpp:14-25, src/curve_mechanism_base.cpp:80-97)
+//      and the replay rule (:98-106, the peer nonce advances before the MAC
+//      check) first, stores the payload while the tag is computed, and a
+//      frame whose tag then fails gets zeros over it before the completion
+//      word -- the batch kernels' order; the caller sees the payload
+//      (verified) or zeros (failed), as after libsodium's verify-then-decrypt
+//      (:226-228).
 // Same bytes, statuses and session-state updates as the batch path with
 // n = 1 (tests/test_gpu_msg.py checks both against the oracle).
 #pragma once
@@ -93,9 +94,9 @@ __device__ __forceinline__ void msg_load_lds(uint8_t *lds, const uint8_t *g, uin
         lds[k] = g[k];
 }
 
+template <uint32_t T = kMsgThreads>
 __device__ __forceinline__ void msg_store_g(uint8_t *g, const uint8_t *lds, uint32_t n, uint32_t tid)
 {
-    constexpr uint32_t T = kMsgThreads;
     const uint32_t head = (4u - ((uint32_t) (uintptr_t) g & 3u)) & 3u;
     const uint32_t h = head < n ? head : n;
     for (uint32_t k = tid; k < h; k += T)
@@ -142,13 +143,38 @@ __device__ __forceinline__ void fe_carry(fe &h)
     h.l[1] += c;
 }
 
-__device__ __forceinline__ fe fe_shfl_down(const fe &x, uint32_t d)
+// x times the element DPP control CTRL brings from another lane; lanes
+// outside ROWS, or whose source lane does not exist, multiply by one.  The
+// steps of an inclusive prefix product over a wave: row_shr 1, 2, 4, 8
+// within rows of 16, then row_bcast 15 and 31 across them (MUL_ROWS 0xa,
+// 0xc) -- DPP moves instead of LDS permutes, so a level costs the multiply.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void fe_mul_dpp(fe &x)
 {
     fe y;
 #pragma unroll
     for (int i = 0; i < 5; ++i)
-        y.l[i] = (uint32_t) __shfl_down((int) x.l[i], d, 64);
-    return y;
+        y.l[i] = (uint32_t) __builtin_amdgcn_update_dpp(i == 0 ? 1 : 0, (int) x.l[i], CTRL, ROWS, 0xf, false);
+    fe_mul(x, y);
+}
+
+// The sum of the wave's elements (limbs below 2^26 + 64, fe_mul's output):
+// 32-bit row sums by DPP (16 of them stay below 2^31), the four rows added in
+// 64 bits and folded back; every lane gets the total.
+__device__ __forceinline__ fe fe_wave_sum(const fe &x)
+{
+    uint64_t w[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        int v = (int) x.l[i];
+        v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true); // row_shr:1
+        v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true); // row_shr:2
+        v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true); // row_shr:4
+        v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true); // row_shr:8
+        w[i] = (uint64_t) (uint32_t) __builtin_amdgcn_readlane(v, 15) + (uint32_t) __builtin_amdgcn_readlane(v, 31) +
+               (uint32_t) __builtin_amdgcn_readlane(v, 47) + (uint32_t) __builtin_amdgcn_readlane(v, 63);
+    }
+    return fe_from_wide(w);
 }
 
 // The launch's completion word: every lane's writes reach memory (system
@@ -240,6 +266,7 @@ template <bool DEC, uint32_t CAP>
 __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d)
 {
     __shared__ uint32_t st_w[kMsgMaxStream / 4 + 16]; // the stream image: 32 bytes, then the message bytes
+    __shared__ uint32_t pt_w[DEC ? kMsgMaxStream / 4 + 16 : 1]; // decode: the plaintext image
     __shared__ int32_t sh_status;
     uint8_t *const st = (uint8_t *) st_w;
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -362,14 +389,23 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
             for (int k = 0; k < 4; ++k)
                 st_w[16u * blk + ((ia + 4u * k) & 15u)] = o[k];
         __syncthreads();
+    } else { // the plaintext image beside the ciphertext (flags byte at stream byte 32, payload after it)
+        if (status == 0 && blk < nb)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                pt_w[16u * blk + ((ia + 4u * k) & 15u)] = o[k];
+        __syncthreads();
     }
 
     // ---- 3. Poly1305 over the ciphertext (stream bytes 32 .. 32+m), wave 0:
-    // c = ceil(N/64) blocks per lane (a Horner sum), nl = ceil(N/c) lanes
-    // right-aligned (zero blocks in front of a Horner sum change nothing);
-    // lane v's sum is worth P_v = (r^c)^(nl-1-v), which a suffix-product scan
-    // over the lanes gives in log2(nl) levels of one multiply each; then the
-    // lanes' terms are summed (tests/test_poly_tree_model.py models it)
+    // c = ceil(N/64) blocks per lane (a Horner sum) over nl = ceil(N/c)
+    // groups of c blocks, group g on lane nl-1-g (the message's last group on
+    // lane 0), with the first group padded by zero blocks in front (zero
+    // blocks ahead of a Horner sum change nothing); lane u's sum is worth
+    // x^u, x = r^c, which an inclusive prefix product over the lanes (one
+    // lane 0, x elsewhere) gives in log2(nl) DPP levels of one multiply each;
+    // then the lanes' terms are summed (tests/test_poly_tree_model.py models
+    // it)
     uint32_t tag[4] = {0, 0, 0, 0};
     if (tid < 64) {
         const fe r = poly_r_from_key(pk[0], pk[1], pk[2], pk[3]);
@@ -379,10 +415,11 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
             ++levels;
         fe h = fe_zero();
         if (lane < nl) {
+            const uint32_t g = nl - 1u - lane;
             const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
 #pragma unroll
             for (uint32_t t = 0; t < 4; ++t) {
-                const int k = (int) (c * lane + t) - (int) pad;
+                const int k = (int) (c * g + t) - (int) pad;
                 if (t < c && k >= 0) {
                     const uint32_t *bp = st_w + 8 + 4 * k;
                     uint32_t b0 = bp[0], b1 = bp[1], b2 = bp[2], b3 = bp[3], hib = 1u << 24;
@@ -412,48 +449,60 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
                 else if (c == 4)
                     fe_mul(x, r2);
             }
-            fe pw = fe_zero();
-            pw.l[0] = 1;
-            if (lane + 1 < nl)
-                pw = x;
-            // (rolled loops: one launch runs them once, from a cold instruction cache)
-#pragma unroll 1
-            for (uint32_t s = 0; s < levels; ++s) {
-                const fe o = fe_shfl_down(pw, 1u << s);
-                if (lane + (1u << s) < nl)
-                    fe_mul(pw, o);
+            fe pw = x;
+            if (lane == 0) {
+                pw = fe_zero();
+                pw.l[0] = 1;
             }
+            fe_mul_dpp<0x111, 0xf>(pw); // row_shr:1
+            if (levels > 1)
+                fe_mul_dpp<0x112, 0xf>(pw); // row_shr:2
+            if (levels > 2)
+                fe_mul_dpp<0x114, 0xf>(pw); // row_shr:4
+            if (levels > 3)
+                fe_mul_dpp<0x118, 0xf>(pw); // row_shr:8
+            if (levels > 4)
+                fe_mul_dpp<0x142, 0xa>(pw); // row_bcast:15
+            if (levels > 5)
+                fe_mul_dpp<0x143, 0xc>(pw); // row_bcast:31
             fe_mul(h, pw);
-#pragma unroll 1
-            for (uint32_t s = 0; s < levels; ++s) {
-                const fe o = fe_shfl_down(h, 1u << s);
-                if (lane + (1u << s) < 64u)
-                    fe_add(h, o);
-                fe_carry(h);
-            }
+            h = fe_wave_sum(h);
         }
         poly_finish(h, pk + 4, tag);
     }
 
-    // ---- 4. results
-    if (!DEC) {
-        if (tid == 0) {
-            st_w[0] = 0x53454d07u; // "\x07MES"
-            st_w[1] = 0x45474153u; // "SAGE"
-            st_w[2] = n0;
-            st_w[3] = n1;
+    // ---- 4. results.  Waves 1-3 store everything but the tag while wave 0
+    // computes it (above), so the stores' round trips to the mapped
+    // destination overlap the MAC instead of following it.
+    // (tag: the same on every lane of wave 0; lane 0's where there was one lane)
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                st_w[4 + k] = tag[k];
+    for (int k = 0; k < 4; ++k)
+        tag[k] = __builtin_amdgcn_readlane(tag[k], 0);
+    if (!DEC) {
+        if (status == 0 && !(ZMQG_MSG_ABLATE & 16)) {
+            if (tid >= 64) {
+                // "\x07MESSAGE" || nonce, then the ciphertext
+                msg_store_g<kMsgThreads - 64>(a.out + 32, st + 32, m, tid - 64);
+                const uint32_t j = tid - 64;
+                if (j < 16) {
+                    const uint32_t w = j < 4 ? 0x53454d07u : j < 8 ? 0x45474153u : j < 12 ? n0 : n1;
+                    a.out[j] = (uint8_t) (w >> (8 * (j & 3u)));
+                }
+            } else if (lane < 16) {
+                const uint32_t w = lane < 4 ? tag[0] : lane < 8 ? tag[1] : lane < 12 ? tag[2] : tag[3];
+                a.out[16 + lane] = (uint8_t) (w >> (8 * (lane & 3u)));
+            }
         }
-        __syncthreads();
-        if (status == 0)
-            if (!(ZMQG_MSG_ABLATE & 16))
-                msg_store_g(a.out, st, end, tid);
         if (tid == 0 && a.status)
             *a.status = status;
         msg_done(a.done);
         return;
+    }
+    const uint32_t P = a.len >= 33u ? a.len - 33u : 0u;
+    const bool spec = status == 0; // header, session and replay checks passed: the payload goes out now
+    if (spec && tid >= 64 && !(ZMQG_MSG_ABLATE & 16)) {
+        msg_store_g<kMsgThreads - 64>(a.out, (const uint8_t *) pt_w + 33, P, tid - 64);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // landed before any zeroing below
     }
     if (tid == 0) {
         if (status == 0) {
@@ -464,19 +513,12 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
     }
     __syncthreads();
     status = sh_status;
-    const uint32_t P = a.len >= 33u ? a.len - 33u : 0u;
     if (status == 0) {
-        // the plaintext image: flags byte at stream byte 32, payload after it
-        if (blk < nb)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                st_w[16u * blk + ((ia + 4u * k) & 15u)] = o[k];
-        __syncthreads();
-        if (!(ZMQG_MSG_ABLATE & 16))
-            msg_store_g(a.out, st + 33, P, tid);
         if (tid == 0)
-            *a.flags_out = st[32] & 3u; // msg_t::more | msg_t::command (curve_mechanism_base.cpp:276)
+            *a.flags_out = ((const uint8_t *) pt_w)[32] & 3u; // msg_t::more | msg_t::command (curve_mechanism_base.cpp:276)
     } else {
+        // a forged frame's speculative payload (or a frame never decrypted)
+        // becomes zeros
         if (!(ZMQG_MSG_ABLATE & 16))
             msg_zero_g(a.out, P, tid);
         if (tid == 0)

@@ -162,3 +162,38 @@ def test_msg_calls_follow_a_batch_on_another_stream(torch_cuda, C):
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0 and torch.equal(back, pay)
     assert dec.get_peer_nonce(0) == 3 + n
+
+
+def test_decode_msg_failed_frame_leaves_the_buffer(torch_cuda, C):
+    """The message kernel stores the payload (into the ctx's staging area)
+    while the tag is computed; a frame whose tag then fails must leave the
+    caller's buffer as it was -- no speculative plaintext and no partial
+    write (zmqg_decode_msg copies the payload out only after a status of 0),
+    as for a frame failing its header checks.  The buffer starts out 0xAA."""
+    import ctypes
+    from libzmq_amd import curve as CC
+    rng = np.random.default_rng(31)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc, dec = _sessions(C, key)
+    nonce = 3
+    for size in (0, 1, 40, 1024, 3000, 3935, 4000, 4063):
+        for where in ("tag", "ciphertext", "command"):
+            pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+            w = bytearray(enc.encode_msg(0, nonce, 0, pay))
+            nonce += 1
+            pos = {"tag": 20, "ciphertext": 33 + size // 2 if size else 32, "command": 2}[where]
+            w[pos] ^= 0x10
+            w = np.frombuffer(bytes(w), np.uint8).copy()
+            out = np.full(size + 64, 0xAA, np.uint8)
+            fl = np.full(1, 7, np.uint8)
+            st = np.zeros(1, np.int32)
+            rc = CC.lib().zmqg_decode_msg(dec._ctx, 0, w.ctypes.data_as(ctypes.c_void_p), len(w),
+                                          out.ctypes.data_as(ctypes.c_void_p), fl.ctypes.data_as(ctypes.c_void_p),
+                                          st.ctypes.data_as(ctypes.c_void_p))
+            exp = C.ERR_UNEXPECTED_COMMAND if where == "command" else C.ERR_CRYPTOGRAPHIC
+            assert rc == 0 and st[0] == exp and fl[0] == 0, (size, where, st[0])
+            assert (out == 0xAA).all(), (size, where)
+    # the session still decodes its next frame
+    pay = b"still in sequence"
+    got, gfl, gst = dec.decode_msg(0, enc.encode_msg(0, nonce, 1, pay))
+    assert gst == 0 and got == pay and gfl == 1

@@ -132,43 +132,84 @@ def test_without_carry_the_fold_wraps():
     assert wrapped > 0
 
 
+def _dpp(vals, ctrl, rows, ident):
+    """One DPP move over a wave of 64 values: row_shr:d (0x110 + d, lane u
+    reads u-d of its row of 16), row_bcast:15 (0x142, lane 15 of each row to
+    the next row) and row_bcast:31 (0x143, lane 31 to rows 2 and 3); lanes
+    outside the row mask or without a source lane get ident."""
+    out = []
+    for u in range(64):
+        row = u >> 4
+        src = None
+        if (rows >> row) & 1:
+            if 0x111 <= ctrl <= 0x11f:
+                d = ctrl - 0x110
+                if (u & 15) >= d:
+                    src = u - d
+            elif ctrl == 0x142 and row > 0:
+                src = 16 * row - 1
+            elif ctrl == 0x143 and row > 1:
+                src = 31
+        out.append(vals[src] if src is not None else ident)
+    return out
+
+
 def prefix_poly(blocks, r):
-    """H = sum m_k r^(N-k) as k_msg computes it since round 4 (before + s):
-    c = ceil(N/64) blocks per lane (Horner), nl = ceil(N/c) lanes
-    right-aligned (zero blocks in front), each lane's Horner value times its
-    power P_v = (r^c)^(nl-1-v) from a suffix-product scan over the lanes
-    (log2 levels of one multiply), then a carried sum over the lanes."""
+    """H = sum m_k r^(N-k) as k_msg computes it (before + s): c = ceil(N/64)
+    blocks per lane (Horner) over nl = ceil(N/c) groups, group g on lane
+    nl-1-g, the first group padded by zero blocks in front; lane u's Horner
+    value times x^u (x = r^c) from an inclusive DPP prefix product over the
+    lanes (one on lane 0, x elsewhere; row_shr 1, 2, 4, 8, row_bcast 15, 31,
+    as many levels as nl needs), then the sum over the lanes: uncarried
+    32-bit row sums (checked below 2^32), the four rows added and folded."""
     n = len(blocks)
     rf = to_fe(r)
     c = (n + 63) // 64
     nl = (n + c - 1) // c
     pad = c * nl - n
+    levels = 0
+    while (1 << levels) < nl:
+        levels += 1
     hs = []
-    for v in range(64):
+    for u in range(64):
         h = [0] * 5
-        if v < nl:
+        if u < nl:
+            g = nl - 1 - u
             for t in range(c):
-                k = c * v + t - pad
+                k = c * g + t - pad
                 if k >= 0:
                     m = to_fe(blocks[k] & ((1 << 128) - 1))
                     m[4] += blocks[k] >> 128 << 24
                     h = fe_mul([h[i] + m[i] for i in range(5)], rf)
         hs.append(h)
+    if levels == 0:
+        return from_fe(hs[0]) % P
     r2 = fe_mul(rf, rf)
     x = [rf, r2, fe_mul(r2, rf), fe_mul(r2, r2)][c - 1]
     one = [1, 0, 0, 0, 0]
-    pw = [x if v < nl - 1 else one for v in range(64)]
-    s = 0
-    while (1 << s) < nl:
-        pw = [fe_mul(pw[v], pw[v + (1 << s)]) if v + (1 << s) < nl else pw[v] for v in range(64)]
-        s += 1
-    terms = [fe_mul(hs[v], pw[v]) if v < nl else [0] * 5 for v in range(64)]
-    d = 1
-    while d < 64:  # the shuffle levels of the sum, each carried
-        terms = [fe_carry([terms[v][i] + (terms[v + d][i] if v + d < 64 else 0) for i in range(5)])
-                 for v in range(64)]
-        d <<= 1
-    return from_fe(terms[0]) % P
+    pw = [one if u == 0 else x for u in range(64)]
+    steps = [(0x111, 0xf), (0x112, 0xf), (0x114, 0xf), (0x118, 0xf), (0x142, 0xa), (0x143, 0xc)]
+    for ctrl, rows in steps[:levels]:
+        limbs = [_dpp([pw[u][i] for u in range(64)], ctrl, rows, 1 if i == 0 else 0) for i in range(5)]
+        pw = [fe_mul(pw[u], [limbs[i][u] for i in range(5)]) for u in range(64)]
+    terms = [fe_mul(hs[u], pw[u]) for u in range(64)]
+    wide = [0] * 5
+    for i in range(5):
+        for row in range(4):
+            rs = sum(terms[u][i] for u in range(16 * row, 16 * row + 16))
+            assert rs < 1 << 31  # the 32-bit DPP row sums cannot wrap
+            wide[i] += rs
+    return from_fe(wide) % P
+
+
+def test_dpp_prefix_is_the_power_of_x():
+    # the DPP steps give lane u the product of lanes 0..u (x^u here)
+    vals = list(range(64))
+    steps = [(0x111, 0xf), (0x112, 0xf), (0x114, 0xf), (0x118, 0xf), (0x142, 0xa), (0x143, 0xc)]
+    for ctrl, rows in steps:
+        o = _dpp(vals, ctrl, rows, 0)
+        vals = [vals[u] + o[u] for u in range(64)]
+    assert vals == [u * (u + 1) // 2 for u in range(64)]
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -176,6 +217,7 @@ def test_prefix_equals_horner(seed):
     rnd = random.Random(100 + seed)
     for _ in range(150):
         r = rnd.getrandbits(128) & 0x0ffffffc0ffffffc0ffffffc0fffffff
-        n = rnd.choice([1, 2, 3, 4, 5, 63, 64, 65, 66, 128, 129, 130, 192, 193, 200, 249, 252, 253, 254])
+        n = rnd.choice([1, 2, 3, 4, 5, 16, 17, 31, 32, 33, 63, 64, 65, 66, 128, 129, 130, 192, 193, 200, 249,
+                          252, 253, 254])
         blocks = [rnd.getrandbits(128) | (1 << 128) for _ in range(n)]
         assert prefix_poly(blocks, r) == horner(blocks, r)
