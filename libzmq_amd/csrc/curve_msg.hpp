@@ -16,9 +16,10 @@
 //   2. the quad of lanes 4b .. 4b+3 computes Salsa20 block b (stream bytes
 //      64b .. 64b+63, salsa20_quad) and each lane XORs its four words;
 //   3. Poly1305 over the ciphertext on wave 0: a Horner sum of c = ceil(N/64)
-//      blocks per lane, each lane's sum times its power of r^c from a DPP
-//      prefix product over the lanes, and a DPP row sum;
-//   4. meanwhile waves 1-3 store encode's "\x07MESSAGE" || BE64(nonce) ||
+//      blocks per lane, each lane's sum times its power of r^c, which wave 3
+//      computes meanwhile by a DPP prefix product over its lanes, and a DPP
+//      row sum;
+//   4. meanwhile waves 1 and 2 store encode's "\x07MESSAGE" || BE64(nonce) ||
 //      ciphertext and wave 0 adds the tag; decode checks the header
 //      (src/mechanism_base.cpp:14-25, src/curve_mechanism_base.cpp:80-97)
 //      and the replay rule (:98-106, the peer nonce advances before the MAC
@@ -268,6 +269,8 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
     __shared__ uint32_t st_w[kMsgMaxStream / 4 + 16]; // the stream image: 32 bytes, then the message bytes
     __shared__ uint32_t pt_w[DEC ? kMsgMaxStream / 4 + 16 : 1]; // decode: the plaintext image
     __shared__ int32_t sh_status;
+    __shared__ uint32_t sh_pk[4];     // Poly1305 r words (wave 0 -> wave 3)
+    __shared__ uint32_t sh_pw[5 * 64]; // lane u's power of r^c, limb-major (wave 3 -> wave 0)
     uint8_t *const st = (uint8_t *) st_w;
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const bool sid_ok = a.sid < a.max_sessions;
@@ -382,6 +385,11 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
             o[k] = (blk == 0 && wi < 8) ? 0u : ((x ^ ks[k]) & mk);
         }
     }
+    if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            sh_pk[k] = pk[k];
+    }
     if (!DEC) { // the ciphertext image replaces the plaintext
         __syncthreads();
         if (blk < nb)
@@ -397,23 +405,27 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
         __syncthreads();
     }
 
-    // ---- 3. Poly1305 over the ciphertext (stream bytes 32 .. 32+m), wave 0:
-    // c = ceil(N/64) blocks per lane (a Horner sum) over nl = ceil(N/c)
-    // groups of c blocks, group g on lane nl-1-g (the message's last group on
-    // lane 0), with the first group padded by zero blocks in front (zero
-    // blocks ahead of a Horner sum change nothing); lane u's sum is worth
-    // x^u, x = r^c, which an inclusive prefix product over the lanes (one
-    // lane 0, x elsewhere) gives in log2(nl) DPP levels of one multiply each;
-    // then the lanes' terms are summed (tests/test_poly_tree_model.py models
-    // it)
-    uint32_t tag[4] = {0, 0, 0, 0};
-    if (tid < 64) {
+    // ---- 3. Poly1305 over the ciphertext (stream bytes 32 .. 32+m): c =
+    // ceil(N/64) blocks per lane (a Horner sum) over nl = ceil(N/c) groups of
+    // c blocks, group g on lane nl-1-g of wave 0 (the message's last group on
+    // lane 0), the first group padded by zero blocks in front (zero blocks
+    // ahead of a Horner sum change nothing); lane u's sum is worth x^u, x =
+    // r^c, which wave 3 computes meanwhile as an inclusive prefix product over
+    // its lanes (one on lane 0, x elsewhere; log2(nl) DPP levels of one
+    // multiply each) and hands over in LDS; wave 0 then sums its lanes' terms
+    // (tests/test_poly_tree_model.py models it).  Waves 1 and 2 store
+    // everything but the tag meanwhile, so the stores' round trips to the
+    // mapped destination overlap the MAC instead of following it.
+    const uint32_t N = (m + 15) >> 4, c = N ? (N + 63) >> 6 : 1u, nl = (N + c - 1) / c, pad = c * nl - N;
+    uint32_t levels = 0;
+    while ((1u << levels) < nl)
+        ++levels;
+    const bool scan = levels && !(ZMQG_MSG_ABLATE & 8);
+    const uint32_t wv = tid >> 6;
+    const uint32_t P = DEC && a.len >= 33u ? a.len - 33u : 0u;
+    fe h = fe_zero();
+    if (wv == 0) {
         const fe r = poly_r_from_key(pk[0], pk[1], pk[2], pk[3]);
-        const uint32_t N = (m + 15) >> 4, c = N ? (N + 63) >> 6 : 1u, nl = (N + c - 1) / c, pad = c * nl - N;
-        uint32_t levels = 0;
-        while ((1u << levels) < nl)
-            ++levels;
-        fe h = fe_zero();
         if (lane < nl) {
             const uint32_t g = nl - 1u - lane;
             const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
@@ -437,7 +449,9 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
                 }
             }
         }
-        if (levels && !(ZMQG_MSG_ABLATE & 8)) {
+    } else if (wv == 3) {
+        if (scan) {
+            const fe r = poly_r_from_key(sh_pk[0], sh_pk[1], sh_pk[2], sh_pk[3]);
             // x = r^c (c uniform, 1..4)
             fe x = r;
             if (c > 1) {
@@ -465,44 +479,54 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
                 fe_mul_dpp<0x142, 0xa>(pw); // row_bcast:15
             if (levels > 5)
                 fe_mul_dpp<0x143, 0xc>(pw); // row_bcast:31
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+                sh_pw[64 * i + lane] = pw.l[i];
+        }
+    } else if (status == 0 && !(ZMQG_MSG_ABLATE & 16)) { // waves 1 and 2
+        const uint32_t j = tid - 64;
+        if (!DEC) {
+            // "\x07MESSAGE" || nonce, then the ciphertext
+            msg_store_g<128>(a.out + 32, st + 32, m, j);
+            if (j < 16) {
+                const uint32_t w = j < 4 ? 0x53454d07u : j < 8 ? 0x45474153u : j < 12 ? n0 : n1;
+                a.out[j] = (uint8_t) (w >> (8 * (j & 3u)));
+            }
+        } else {
+            // header, session and replay checks passed: the payload goes out
+            // now, and is zeroed below if the tag fails
+            msg_store_g<128>(a.out, (const uint8_t *) pt_w + 33, P, j);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // landed before any zeroing below
+        }
+    }
+    __syncthreads();
+    uint32_t tag[4] = {0, 0, 0, 0};
+    if (wv == 0) {
+        if (scan) {
+            fe pw;
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+                pw.l[i] = sh_pw[64 * i + lane];
             fe_mul(h, pw);
             h = fe_wave_sum(h);
         }
         poly_finish(h, pk + 4, tag);
+        // (the same on every lane; lane 0's where there was one lane)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            tag[k] = __builtin_amdgcn_readlane(tag[k], 0);
     }
 
-    // ---- 4. results.  Waves 1-3 store everything but the tag while wave 0
-    // computes it (above), so the stores' round trips to the mapped
-    // destination overlap the MAC instead of following it.
-    // (tag: the same on every lane of wave 0; lane 0's where there was one lane)
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        tag[k] = __builtin_amdgcn_readlane(tag[k], 0);
+    // ---- 4. results
     if (!DEC) {
-        if (status == 0 && !(ZMQG_MSG_ABLATE & 16)) {
-            if (tid >= 64) {
-                // "\x07MESSAGE" || nonce, then the ciphertext
-                msg_store_g<kMsgThreads - 64>(a.out + 32, st + 32, m, tid - 64);
-                const uint32_t j = tid - 64;
-                if (j < 16) {
-                    const uint32_t w = j < 4 ? 0x53454d07u : j < 8 ? 0x45474153u : j < 12 ? n0 : n1;
-                    a.out[j] = (uint8_t) (w >> (8 * (j & 3u)));
-                }
-            } else if (lane < 16) {
-                const uint32_t w = lane < 4 ? tag[0] : lane < 8 ? tag[1] : lane < 12 ? tag[2] : tag[3];
-                a.out[16 + lane] = (uint8_t) (w >> (8 * (lane & 3u)));
-            }
+        if (status == 0 && !(ZMQG_MSG_ABLATE & 16) && tid < 16) {
+            const uint32_t w = tid < 4 ? tag[0] : tid < 8 ? tag[1] : tid < 12 ? tag[2] : tag[3];
+            a.out[16 + tid] = (uint8_t) (w >> (8 * (tid & 3u)));
         }
         if (tid == 0 && a.status)
             *a.status = status;
         msg_done(a.done);
         return;
-    }
-    const uint32_t P = a.len >= 33u ? a.len - 33u : 0u;
-    const bool spec = status == 0; // header, session and replay checks passed: the payload goes out now
-    if (spec && tid >= 64 && !(ZMQG_MSG_ABLATE & 16)) {
-        msg_store_g<kMsgThreads - 64>(a.out, (const uint8_t *) pt_w + 33, P, tid - 64);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // landed before any zeroing below
     }
     if (tid == 0) {
         if (status == 0) {
