@@ -310,7 +310,17 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
             msg_inline_lds(st, d, L, tid);
         else if (!(ZMQG_MSG_ABLATE & 32))
             msg_load_lds(st, a.in, L, tid);
-        __syncthreads();
+        m = L >= 33u ? L - 32u : 0u;
+    }
+    // zero the bytes after the message up to the next 16-byte block (Poly1305
+    // pads a partial last block with zeros; below a 33-byte frame, bytes 32..
+    // -- past the message either way)
+    const uint32_t end = 32 + m;
+    if (tid < 16 && end + tid < kMsgMaxStream + 64)
+        st[end + tid] = 0;
+    __syncthreads();
+    if (DEC) {
+        const uint32_t L = a.len;
         // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
         const uint32_t b0 = L ? st[0] : 0u;
         const uint32_t w0 = L >= 8 ? st_w[0] : 0u, w1 = L >= 8 ? st_w[1] : 0u;
@@ -322,7 +332,6 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
             status = ZMQG_ERR_MALFORMED_MESSAGE;
         if (!sid_ok)
             status = ZMQG_ERR_SESSION;
-        m = L >= 33u ? L - 32u : 0u;
         if (status == 0) {
             n0 = st_w[2];
             n1 = st_w[3];
@@ -333,12 +342,6 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
                 status = ZMQG_ERR_INVALID_SEQUENCE;
         }
     }
-    // zero the bytes after the message up to the next 16-byte block (Poly1305
-    // pads a partial last block with zeros)
-    const uint32_t end = 32 + m;
-    if (tid < 16 && end + tid < kMsgMaxStream + 64)
-        st[end + tid] = 0;
-    __syncthreads();
     if (DEC && status == 0 && tid == 0)
         a.peer[a.sid] = nc;
 
