@@ -112,9 +112,10 @@ __device__ __forceinline__ void msg_store_g(uint8_t *g, const uint8_t *lds, uint
         g[k] = lds[k];
 }
 
+template <uint32_t T = kMsgThreads>
 __device__ __forceinline__ void msg_zero_g(uint8_t *g, uint32_t n, uint32_t tid)
 {
-    for (uint32_t k = tid; k < n; k += kMsgThreads)
+    for (uint32_t k = tid; k < n; k += T)
         g[k] = 0;
 }
 
@@ -268,7 +269,6 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
 {
     __shared__ uint32_t st_w[kMsgMaxStream / 4 + 16]; // the stream image: 32 bytes, then the message bytes
     __shared__ uint32_t pt_w[DEC ? kMsgMaxStream / 4 + 16 : 1]; // decode: the plaintext image
-    __shared__ int32_t sh_status;
     __shared__ uint32_t sh_pk[4];     // Poly1305 r words (wave 0 -> wave 3)
     __shared__ uint32_t sh_pw[5 * 64]; // lane u's power of r^c, limb-major (wave 3 -> wave 0)
     uint8_t *const st = (uint8_t *) st_w;
@@ -531,28 +531,20 @@ __global__ __launch_bounds__(kMsgThreads) void k_msg(MsgArgs a, MsgInline<CAP> d
         msg_done(a.done);
         return;
     }
-    if (tid == 0) {
-        if (status == 0) {
-            if ((tag[0] ^ st_w[4]) | (tag[1] ^ st_w[5]) | (tag[2] ^ st_w[6]) | (tag[3] ^ st_w[7]))
-                status = ZMQG_ERR_CRYPTOGRAPHIC;
+    // wave 0 decides: the tag check, and zeros over a forged frame's payload
+    // (waves 1 and 2 drained their speculative stores before the barrier
+    // above, so these land after them)
+    if (wv == 0) {
+        if (status == 0 && ((tag[0] ^ st_w[4]) | (tag[1] ^ st_w[5]) | (tag[2] ^ st_w[6]) | (tag[3] ^ st_w[7])))
+            status = ZMQG_ERR_CRYPTOGRAPHIC; // src/curve_mechanism_base.cpp:277-281
+        if (status != 0 && !(ZMQG_MSG_ABLATE & 16))
+            msg_zero_g<64>(a.out, P, lane);
+        if (tid == 0) {
+            // msg_t::more | msg_t::command (curve_mechanism_base.cpp:276)
+            *a.flags_out = status == 0 ? ((const uint8_t *) pt_w)[32] & 3u : 0u;
+            *a.status = status;
         }
-        sh_status = status;
     }
-    __syncthreads();
-    status = sh_status;
-    if (status == 0) {
-        if (tid == 0)
-            *a.flags_out = ((const uint8_t *) pt_w)[32] & 3u; // msg_t::more | msg_t::command (curve_mechanism_base.cpp:276)
-    } else {
-        // a forged frame's speculative payload (or a frame never decrypted)
-        // becomes zeros
-        if (!(ZMQG_MSG_ABLATE & 16))
-            msg_zero_g(a.out, P, tid);
-        if (tid == 0)
-            *a.flags_out = 0;
-    }
-    if (tid == 0)
-        *a.status = status;
     msg_done(a.done);
 }
 
