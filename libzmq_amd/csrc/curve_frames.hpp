@@ -1077,6 +1077,65 @@ __device__ __forceinline__ void frame_load_exact(uint64_t A4, uint32_t lim, uint
 }
 
 // ---------------------------------------------------------------- one lane per frame
+// Wave-wide reductions and scans of the frame kernels' prologue on DPP
+// moves instead of LDS permutes (row_shr 1, 2, 4, 8 within rows of 16, then
+// row_bcast 15 and 31, or readlanes of the row results): a level costs a
+// couple of VALU cycles instead of an LDS round trip.  Lanes without a
+// source read 0, the identity of an unsigned maximum.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v)
+{
+    const uint32_t lo = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) (uint32_t) v, CTRL, ROWS, 0xf, true);
+    const uint32_t hi = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) (uint32_t) (v >> 32), CTRL, ROWS, 0xf, true);
+    return ((unsigned long long) hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long max_u64(unsigned long long a, unsigned long long b)
+{
+    return a > b ? a : b;
+}
+// inclusive prefix maximum over the wave's lanes
+__device__ __forceinline__ unsigned long long wave_scan_max_u64(unsigned long long v)
+{
+    v = max_u64(v, dpp_u64<0x111, 0xf>(v)); // row_shr:1
+    v = max_u64(v, dpp_u64<0x112, 0xf>(v)); // row_shr:2
+    v = max_u64(v, dpp_u64<0x114, 0xf>(v)); // row_shr:4
+    v = max_u64(v, dpp_u64<0x118, 0xf>(v)); // row_shr:8
+    v = max_u64(v, dpp_u64<0x142, 0xa>(v)); // row_bcast:15
+    v = max_u64(v, dpp_u64<0x143, 0xc>(v)); // row_bcast:31
+    return v;
+}
+// the previous lane's value (lane 0: 0)
+__device__ __forceinline__ unsigned long long wave_prev_u64(unsigned long long v)
+{
+    return dpp_u64<0x138, 0xf>(v); // wave_shr:1
+}
+// the wave's maximum, on every lane
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
+{
+    v = max_u64(v, dpp_u64<0x111, 0xf>(v));
+    v = max_u64(v, dpp_u64<0x112, 0xf>(v));
+    v = max_u64(v, dpp_u64<0x114, 0xf>(v));
+    v = max_u64(v, dpp_u64<0x118, 0xf>(v));
+    unsigned long long m = 0;
+#pragma unroll
+    for (int r = 15; r < 64; r += 16) {
+        const unsigned long long x = ((unsigned long long) (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (v >> 32), r) << 32) |
+                                     (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) v, r);
+        m = max_u64(m, x);
+    }
+    return m;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+    auto mx = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+    v = mx(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x111, 0xf, 0xf, true));
+    v = mx(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x112, 0xf, 0xf, true));
+    v = mx(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x114, 0xf, 0xf, true));
+    v = mx(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, true));
+    return mx(mx((uint32_t) __builtin_amdgcn_readlane((int) v, 15), (uint32_t) __builtin_amdgcn_readlane((int) v, 31)),
+              mx((uint32_t) __builtin_amdgcn_readlane((int) v, 47), (uint32_t) __builtin_amdgcn_readlane((int) v, 63)));
+}
+
 // Sequential frame kernel: one lane owns one frame and walks its keystream
 // windows in order (64 frames per wave), with Poly1305 in the sequential
 // radix-2^32 form (curve_device.hpp poly32_*): no powers of r, no
@@ -1236,14 +1295,8 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
                 rp.iota[i] = i;
         }
         if (lb) {
-            unsigned long long sc = vn;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const unsigned long long o = __shfl_up(sc, d);
-                if ((int) lane >= d)
-                    sc = o > sc ? o : sc;
-            }
-            const unsigned long long up = __shfl_up(sc, 1);
+            const unsigned long long sc = wave_scan_max_u64(vn);
+            const unsigned long long up = wave_prev_u64(sc);
             if (lane == 63)
                 sh_wmax[threadIdx.x >> 6] = sc;
             __syncthreads();
@@ -1263,22 +1316,11 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
     if (!small)
         S = 0;
     const uint32_t nw = (S + 63u) >> 6;
-    uint32_t mx = nw;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(mx, d);
-        mx = o > mx ? o : mx;
-    }
-    const uint32_t steps = __builtin_amdgcn_readfirstlane(mx);
+    const uint32_t steps = __builtin_amdgcn_readfirstlane(wave_max_u32(nw));
     const uint32_t v = (uint32_t) A & 3u;
     const uint64_t A4 = A & ~3ull;
     const uint32_t lim = S + v; // stream words whose first byte is below lim hold a stream byte
-    uint64_t wave_end = nw ? A + S : 0; // end of the wave's furthest frame: reads below it stay in the buffer
-#pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-        const uint64_t o = __shfl_xor(wave_end, sh);
-        wave_end = o > wave_end ? o : wave_end;
-    }
+    const uint64_t wave_end = wave_max_u64(nw ? A + S : 0); // end of the wave's furthest frame: reads below it stay in the buffer
     // window 1's words (word 0 is window 0's word 16, d0); windows t and t+1
     // alternate between the two buffers
     uint32_t ddA[16], ddB[16];

@@ -212,14 +212,8 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
                 rp.iota[i] = i;
         }
         if (lb) {
-            unsigned long long sc = vn;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const unsigned long long o = __shfl_up(sc, d);
-                if ((int) lane >= d)
-                    sc = o > sc ? o : sc;
-            }
-            const unsigned long long up = __shfl_up(sc, 1);
+            const unsigned long long sc = wave_scan_max_u64(vn);
+            const unsigned long long up = wave_prev_u64(sc);
             if (lane == 63)
                 sh_wmax[wv] = sc;
             __syncthreads();
@@ -238,13 +232,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     if (!small)
         S = 0;
     const uint32_t nw = (S + 63u) >> 6;
-    uint32_t mx = nw;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t o = __shfl_xor(mx, d);
-        mx = o > mx ? o : mx;
-    }
-    const uint32_t steps = __builtin_amdgcn_readfirstlane(mx);
+    const uint32_t steps = __builtin_amdgcn_readfirstlane(wave_max_u32(nw));
 
     // ---- the wave's staging areas and its lanes' share of the cooperative moves
     uint8_t *const wlds = st_lds + wv * kStWave;
