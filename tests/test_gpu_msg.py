@@ -197,3 +197,38 @@ def test_decode_msg_failed_frame_leaves_the_buffer(torch_cuda, C):
     pay = b"still in sequence"
     got, gfl, gst = dec.decode_msg(0, enc.encode_msg(0, nonce, 1, pay))
     assert gst == 0 and got == pay and gfl == 1
+
+
+def _msg_poly_shape(stream_len):
+    """(c, nl, levels) of k_msg's Poly1305 for a message of stream_len bytes
+    after the 32-byte key (curve_msg.hpp, step 3)."""
+    n = (stream_len + 15) // 16
+    c = (n + 63) // 64 if n else 1
+    nl = (n + c - 1) // c
+    levels = 0
+    while (1 << levels) < nl:
+        levels += 1
+    return c, nl, levels
+
+
+def test_msg_poly_every_lane_shape(torch_cuda, C):
+    """Payload sizes chosen so that k_msg's Poly1305 runs every shape it has:
+    c = 1..4 blocks per lane (x = r, r^2, r^3, r^4) and 0..6 DPP prefix
+    levels (row_shr 1-8, row_bcast 15 and 31), each at both ends of its
+    range -- encode against the oracle, then decode back."""
+    rng = np.random.default_rng(41)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc, dec = _sessions(C, key)
+    # ciphertext m = 1 + P bytes (flags byte, no SUBSCRIBE/CANCEL prefix)
+    sizes = sorted({0, 15, 16, 31, 32, 47, 48, 63, 64, 127, 128, 129, 255, 256, 257, 500, 511, 512, 513, 767,
+                    1000, 1023, 1024, 1025, 1500, 2047, 2048, 2049, 2500, 3000, 3071, 3072, 3073, 3500, 3935})
+    shapes = {_msg_poly_shape(1 + p)[0::2] for p in sizes}
+    assert {(c, lv) for c in (1, 2, 3, 4) for lv in range(7) if c == 1 or lv == 6} <= shapes | {(1, 0)}
+    nonce = 3
+    for p in sizes:
+        pay = rng.integers(0, 256, p, dtype=np.uint8).tobytes()
+        w = enc.encode_msg(0, nonce, 1, pay)
+        assert w == _oracle_wire(key, nonce, 1, pay), (p, _msg_poly_shape(1 + p))
+        got, gfl, gst = dec.decode_msg(0, w)
+        assert gst == 0 and got == pay and gfl == 1, (p, gst)
+        nonce += 1
