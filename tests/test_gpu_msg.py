@@ -232,3 +232,43 @@ def test_msg_poly_every_lane_shape(torch_cuda, C):
         got, gfl, gst = dec.decode_msg(0, w)
         assert gst == 0 and got == pay and gfl == 1, (p, gst)
         nonce += 1
+
+
+def test_decode_msg_random_tampering_matches_oracle(torch_cuda, C):
+    """Random sizes across every inline class and the memory route, random
+    flags, and for most frames one flipped bit at a random wire position (or
+    a truncation): each frame's status, flags and payload equal the oracle's
+    sequential decode of the same sequence (src/curve_mechanism_base.cpp:
+    80-284), peer-nonce advance included."""
+    rng = np.random.default_rng(77)
+    key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    enc, dec = _sessions(C, key)
+    seq, nonce = [], 3
+    for _ in range(160):
+        size = int(rng.choice([rng.integers(0, 64), rng.integers(64, 1100), rng.integers(1100, 4064)]))
+        flags = int(rng.integers(0, 4))
+        w = bytearray(enc.encode_msg(0, nonce, flags, rng.integers(0, 256, size, dtype=np.uint8).tobytes()))
+        nonce += int(rng.choice([1, 1, 1, 2]))
+        r = rng.random()
+        if r < 0.6:
+            pos = int(rng.integers(0, len(w)))
+            w[pos] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.7:
+            w = w[:int(rng.integers(0, len(w)))]
+        seq.append(bytes(w))
+        if rng.random() < 0.05 and len(seq) > 2:  # a replay of an earlier frame
+            seq.append(seq[int(rng.integers(0, len(seq) - 1))])
+    wl = np.array([len(w) for w in seq], np.uint32)
+    woff = np.concatenate([[0], np.cumsum(wl[:-1])]).astype(np.uint64)
+    wire = np.frombuffer(b"".join(seq) + b"\0" * 64, np.uint8)
+    pout = np.concatenate([[0], np.cumsum([max(len(w) - 33, 0) for w in seq][:-1])]).astype(np.uint64)
+    sess = O.make_sessions([key], dec_prefix=O.CLIENT_PREFIX)
+    peer = np.array([2], np.uint64)
+    out, fl, st = O.decode_batch(sess, peer, np.zeros(len(seq), np.uint32), woff, wl, wire, pout,
+                                 int(pout[-1]) + len(seq[-1]) + 1)
+    for i, w in enumerate(seq):
+        got, gfl, gst = dec.decode_msg(0, w)
+        assert gst == int(st[i]), (i, len(w), gst, int(st[i]))
+        if gst == 0:
+            assert got == bytes(out[int(pout[i]):int(pout[i]) + len(w) - 33]) and gfl == int(fl[i]), i
+    assert dec.get_peer_nonce(0) == int(peer[0])
