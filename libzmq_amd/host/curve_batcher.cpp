@@ -138,6 +138,7 @@ int curve_batcher_t::open_slot (kind_t kind_, size_t in_need_, size_t out_need_)
         _free.pop_back ();
         s->kind = kind_;
         s->n = s->in_used = s->out_used = 0;
+        s->max_len = 0;
         _open[kind_] = s;
     }
     return 0;
@@ -171,6 +172,8 @@ int curve_batcher_t::submit_encode (curve_encoding_gpu_t *conn_,
     s->len[i] = static_cast<uint32_t> (size_);
     s->out_off[i] = s->out_used;
     s->tags[i] = tag_;
+    if (size_ > s->max_len)
+        s->max_len = size_;
     if (size_)
         memcpy (s->in + s->in_used, data_, size_);
     s->in_used += size_;
@@ -205,6 +208,8 @@ int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
     s->len[i] = static_cast<uint32_t> (size_);
     s->out_off[i] = s->in_used + 33;
     s->tags[i] = tag_;
+    if (size_ > s->max_len)
+        s->max_len = size_;
     if (size_)
         memcpy (s->in + s->in_used, wire_, size_);
     s->in_used += size_;
@@ -214,17 +219,21 @@ int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
 int curve_batcher_t::launch (slot_t *s)
 {
     int rc;
+    //  the slot's longest frame bounds the batch: a slot of small messages
+    //  (every stream within the frame kernel's 4.5 KiB) skips the
+    //  large-frame launches
+    zmqg_batch_opts o;
+    memset (&o, 0, sizeof o);
+    o.size = sizeof o;
+    o.max_len = s->max_len ? s->max_len : 1;
     if (s->kind == encode_kind)
-        rc = zmqg_encode_batch (_ctx, s->n, s->sid, s->nonce, s->flags,
-                                s->in_off, s->len, s->in, s->out_off, s->out,
-                                _stream);
+        rc = zmqg_encode_batch_ex (_ctx, s->n, s->sid, s->nonce, s->flags,
+                                   s->in_off, s->len, s->in, s->out_off,
+                                   s->out, &o, _stream);
     else {
         //  the slot is host memory the I/O thread can read while the batch
         //  runs: verify before any plaintext reaches it, as libsodium's open
         //  does (src/curve_mechanism_base.cpp:226-228)
-        zmqg_batch_opts o;
-        memset (&o, 0, sizeof o);
-        o.size = sizeof o;
         o.flags = _config.verify_first ? ZMQG_OPT_VERIFY_FIRST : 0;
         o.out_bytes = s->in_used;
         rc = zmqg_decode_batch_ex (_ctx, s->n, s->sid, s->in_off, s->len,

@@ -146,6 +146,7 @@ class curve_batcher_t
         std::vector<uint64_t> tags;
         kind_t kind;
         size_t n, in_used, out_used;
+        uint64_t max_len; //  longest payload (encode) / wire frame (decode) so far
         uint64_t fence;
     };
 
