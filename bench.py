@@ -258,38 +258,55 @@ def main():
     # traffic: HBM read bytes per launch of the same kernel from the committed
     # PMC pass (FETCH_SIZE, doubled per the gfx950 note in MI355X_MICROARCH.md);
     # the write side is reported beside it
-    traffic = traffic_write = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic_config2.json")
-    if os.path.exists(pmc) and n == 65536 and P == 1024:
+    # PMC files count only when they measured THIS library: each carries the
+    # source id (zmqg_build_id) of the build its passes loaded
+    src_id, commit = C.build_id()
+    pmc_notes = {}
+
+    def pmc_file(name):
+        path = os.path.join(ROOT, "profiles", name)
+        if not (os.path.exists(path) and n == 65536 and P == 1024):
+            pmc_notes[name] = "absent"
+            return None
         try:
-            d = json.load(open(pmc))
-            if d.get("kernel") == ROOF_KERNEL:
-                traffic = d.get("read_bytes_per_launch")
-                traffic_write = d.get("write_bytes_per_launch")
+            d = json.load(open(path))
         except Exception:
-            traffic = traffic_write = None
+            pmc_notes[name] = "unreadable"
+            return None
+        if d.get("kernel") != ROOF_KERNEL:
+            pmc_notes[name] = "other kernel"
+            return None
+        if d.get("source_id") != src_id:
+            pmc_notes[name] = f"measured build {d.get('source_id')}, loaded {src_id}: not used"
+            return None
+        pmc_notes[name] = f"build {src_id} (commit {d.get('commit')})"
+        return d
+
+    traffic = traffic_write = None
+    d = pmc_file("pmc_traffic_config2.json")
+    if d:
+        traffic = d.get("read_bytes_per_launch")
+        traffic_write = d.get("write_bytes_per_launch")
     # The kernel is VALU-issue bound: its VALU
     # instruction count per launch (committed PMC pass) over the same live
     # launch duration, against the chip's VALU issue peak (1024 SIMDs x 16
     # lanes per cycle) at the spec clock and at the clock measured under
     # this load.
     valu = None
-    pv = os.path.join(ROOT, "profiles", "pmc_valu_config2.json")
-    if os.path.exists(pv) and n == 65536 and P == 1024 and dec_avg_s > 0:
+    d = pmc_file("pmc_valu_config2.json")
+    if d and dec_avg_s > 0:
         try:
-            d = json.load(open(pv))
-            if d.get("kernel") == ROOF_KERNEL:
-                ops = d["valu_wave_instr_per_launch"] * 64 / dec_avg_s
-                peak = d["simds"] * d["lanes_per_simd_per_cycle"] * d["clock_ghz_spec"] * 1e9
-                peak_m = d["simds"] * d["lanes_per_simd_per_cycle"] * d["clock_ghz_measured"] * 1e9
-                valu = {"achieved": ops / 1e12, "peak": peak / 1e12, "unit": "T lane-ops/s", "frac": ops / peak,
-                        "frac_at_measured_clock": ops / peak_m, "clock_ghz_measured": d["clock_ghz_measured"],
-                        "lane_ops_per_frame": d["valu_lane_ops_per_frame"]}
-        except Exception:
+            ops = d["valu_wave_instr_per_launch"] * 64 / dec_avg_s
+            peak = d["simds"] * d["lanes_per_simd_per_cycle"] * d["clock_ghz_spec"] * 1e9
+            peak_m = d["simds"] * d["lanes_per_simd_per_cycle"] * d["clock_ghz_measured"] * 1e9
+            valu = {"achieved": ops / 1e12, "peak": peak / 1e12, "unit": "T lane-ops/s", "frac": ops / peak,
+                    "frac_at_measured_clock": ops / peak_m, "clock_ghz_measured": d["clock_ghz_measured"],
+                    "lane_ops_per_frame": d["valu_lane_ops_per_frame"]}
+        except (KeyError, TypeError):
             valu = None
     roofline = {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBPS) if achieved else None, "traffic": traffic,
-                "traffic_write": traffic_write, "valu": valu,
+                "traffic_write": traffic_write, "valu": valu, "pmc_files": pmc_notes,
                 "algorithmic_bytes_per_launch": dec_read, "avg_launch_us": dec_avg_s * 1e6,
                 "encode_main_avg_us": enc_avg_s * 1e6,
                 "encode_call_avg_us": enc_call_ms / max(enc_body_n, 1) * 1e3,
@@ -320,6 +337,7 @@ def main():
                    "frames_per_gpu": n, "payload_bytes": P, "wire_bytes": W, "sessions": 1,
                    "parallelism": f"frame-sharded x{world}, no collective"},
         "roofline": roofline,
+        "build": {"source_id": src_id, "commit": commit},
     }
 
     if not args.no_configs:

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define ZMQG_CURVE_ABI_VERSION 4
+#define ZMQG_CURVE_ABI_VERSION 5
 
 /* Per-frame status codes, identical to include/zmq.h:424-437. */
 #define ZMQG_STATUS_OK 0
@@ -327,6 +327,25 @@ int zmqg_fence_record(zmqg_ctx *ctx, void *stream, uint64_t *fence_out);
 int zmqg_fence_query(zmqg_ctx *ctx, uint64_t fence);
 int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
 
+/* Completion wake-up for a sleeping I/O thread.  The reference's I/O thread
+ * sleeps in epoll_wait (src/epoll.cpp:157-158) and is woken only by a file
+ * descriptor it watches -- its mailbox's eventfd (src/io_thread.cpp:54,
+ * src/signaler.cpp) or a socket; an engine with nothing to write has reset
+ * POLLOUT (src/stream_engine_base.cpp:350-353) and resumes only through
+ * restart_output / restart_input (:383-390, :400-442).
+ *
+ * zmqg_fence_record_notify is zmqg_fence_record plus a wake-up: once the
+ * stream has passed the fence, an 8-byte 1 is written to `fd` (eventfd
+ * counter semantics; a pipe's write end works too) from a HIP runtime thread,
+ * and from then on zmqg_fence_query of that fence returns 1.  The poller
+ * watches `fd` for POLLIN, reads it, and polls its fences.  `fd` must stay
+ * open until zmqg_notify_quiesce has returned: that call waits until every
+ * notification enqueued on the ctx so far has been delivered (the streams
+ * must be able to reach them).  zmqg_ctx_destroy waits for them too.
+ * (Replaces no reference symbol: the reference codec is synchronous.) */
+int zmqg_fence_record_notify(zmqg_ctx *ctx, void *stream, int fd, uint64_t *fence_out);
+int zmqg_notify_quiesce(zmqg_ctx *ctx);
+
 /* ZMTP framing on the device.
  *
  * zmqg_encode_zmtp: zmqg_encode_batch plus the engine's ZMTP encoder
@@ -473,6 +492,14 @@ int zmqg_ctx_get_profile(zmqg_ctx *ctx, int kind, double *ms_total, uint64_t *la
 
 /* Text for the last HIP error seen by this ctx (static storage). */
 const char *zmqg_last_error(zmqg_ctx *ctx);
+
+/* Build identity, "<source id> <commit>": the first 16 hex digits of the
+ * SHA-256 of the library's sources (the .hip and .hpp files of libzmq_amd/csrc and this
+ * header, in name order) and the git commit the tree was at when it was
+ * built.  Measurement files under profiles/ carry the source id of the
+ * library they measured; bench.py folds them into its line only when it
+ * equals the loaded library's. */
+const char *zmqg_build_id(void);
 
 #ifdef __cplusplus
 }

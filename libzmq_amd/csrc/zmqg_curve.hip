@@ -37,6 +37,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <vector>
@@ -216,7 +220,11 @@ struct zmqg_ctx {
     uint8_t *dbuf = nullptr;
     size_t dbuf_bytes = 0;
     hipStream_t own_stream = nullptr;
-    hipStream_t last_stream = nullptr; // the stream of the last batch call (peer-nonce accessors order after it)
+    // the stream of the last batch call (the session accessors and the
+    // per-message calls order after it); has_last tells "none yet" from the
+    // null stream, which is a stream like any other here
+    hipStream_t last_stream = nullptr;
+    bool has_last = false;
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
@@ -228,6 +236,12 @@ struct zmqg_ctx {
     // events recycled through fence_pool
     std::vector<std::pair<uint64_t, hipEvent_t>> fences;
     std::vector<hipEvent_t> fence_pool;
+    // zmqg_fence_record_notify: ids whose host function has run (a fence
+    // found there is reached whatever its event says), and the host
+    // functions enqueued and not yet finished
+    std::mutex notify_mu;
+    std::vector<uint64_t> notified;
+    std::atomic<int> notify_pending{0};
     uint64_t fence_ctr = 0;
     std::mutex fence_mu;
     char last_error[256] = {0};
@@ -243,6 +257,29 @@ struct zmqg_ctx {
             return -EIO;                                                               \
         }                                                                                      \
     } while (0)
+
+// The ctx's work is ordered by stream: a batch call runs on the caller's
+// stream (which then becomes the ctx's last stream); a call that switches
+// to another stream first makes it wait for everything queued on the last
+// one (an event recorded there).  The null stream is a stream like any
+// other: with own_stream non-blocking it is not ordered implicitly.
+static void set_last(zmqg_ctx *ctx, hipStream_t st)
+{
+    ctx->last_stream = st;
+    ctx->has_last = true;
+}
+
+static int order_after_last(zmqg_ctx *ctx, hipStream_t st)
+{
+    if (ctx->has_last && ctx->last_stream != st) {
+        if (!ctx->order_ev)
+            ZCHECK(ctx, hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
+        ZCHECK(ctx, hipEventRecord(ctx->order_ev, ctx->last_stream));
+        ZCHECK(ctx, hipStreamWaitEvent(st, ctx->order_ev, 0));
+    }
+    set_last(ctx, st);
+    return 0;
+}
 
 // =====================================================================
 // device helpers
@@ -2335,7 +2372,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
         return -EINVAL;
     (void) hipSetDevice(ctx->device);
     // the ctx's work is on its last batch stream and its own stream
-    if (ctx->last_stream)
+    if (ctx->has_last && ctx->last_stream != ctx->own_stream)
         (void) hipStreamSynchronize(ctx->last_stream);
     if (ctx->own_stream)
         (void) hipStreamSynchronize(ctx->own_stream);
@@ -2368,6 +2405,9 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
         (void) hipHostFree(ctx->sinst);
     if (ctx->order_ev)
         (void) hipEventDestroy(ctx->order_ev);
+    // notification host functions still queued hold the ctx
+    while (ctx->notify_pending.load(std::memory_order_acquire) > 0)
+        sched_yield();
     if (ctx->own_stream)
         (void) hipStreamDestroy(ctx->own_stream);
     for (auto &v : ctx->prof)
@@ -2455,6 +2495,11 @@ int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], cons
     in[17] = (uint32_t) peer_nonce;
     in[18] = (uint32_t) (peer_nonce >> 32);
     ctx->h_downgrade[sid] = downgrade_sub ? 1 : 0;
+    // after whatever the ctx queued on its last stream (an earlier
+    // asynchronous install of the same sid, frames still using its keys)
+    int orc = order_after_last(ctx, ctx->own_stream);
+    if (orc)
+        return orc;
     uint32_t *d = nullptr;
     ZCHECK(ctx, hipMalloc((void **) &d, sizeof in));
     hipError_t e = hipMemcpyAsync(d, in, sizeof in, hipMemcpyHostToDevice, ctx->own_stream);
@@ -2522,7 +2567,11 @@ int zmqg_session_set_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const
     memcpy(pfx.w, enc_prefix, 16);
     memcpy(pfx.w + 4, dec_prefix, 16);
     hipStream_t st = (hipStream_t) stream;
-    ctx->last_stream = st;
+    // the install overwrites sessions that work queued on the previous
+    // stream may still be using: it runs after that work
+    int orc = order_after_last(ctx, st);
+    if (orc)
+        return orc;
     hipLaunchKernelGGL(k_session_setup_batch, dim3((uint32_t) ((n + 255) / 256)), dim3(256), 0, st, (uint32_t) n,
                        (const uint8_t *) ctx->sinst_dev, (const uint32_t *) precom, pfx, ctx->sessions, ctx->peer,
                        ctx->send);
@@ -2538,7 +2587,7 @@ static int session_u64_set(zmqg_ctx *ctx, unsigned long long *arr, uint32_t sid,
     if (!ctx || sid >= ctx->max_sessions)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->own_stream;
+    hipStream_t st = ctx->has_last ? ctx->last_stream : ctx->own_stream;
     hipLaunchKernelGGL(k_set_peer, dim3(1), dim3(64), 0, st, arr, sid, (unsigned long long) v);
     ZCHECK(ctx, hipGetLastError());
     ZCHECK(ctx, hipStreamSynchronize(st));
@@ -2550,7 +2599,7 @@ static int session_u64_get(zmqg_ctx *ctx, const unsigned long long *arr, uint32_
     if (!ctx || sid >= ctx->max_sessions || !out)
         return -EINVAL;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = ctx->last_stream ? ctx->last_stream : ctx->own_stream;
+    hipStream_t st = ctx->has_last ? ctx->last_stream : ctx->own_stream;
     unsigned long long v = 0;
     ZCHECK(ctx, hipMemcpyAsync(&v, arr + sid, sizeof v, hipMemcpyDeviceToHost, st));
     ZCHECK(ctx, hipStreamSynchronize(st));
@@ -2647,7 +2696,7 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         return -EINVAL;
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    ctx->last_stream = st;
+    set_last(ctx, st);
     int rc = ensure_workspace(ctx, n, st);
     if (rc)
         return rc;
@@ -2720,7 +2769,7 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     const uint64_t out_bytes = opt_out_bytes(opts);
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    ctx->last_stream = st;
+    set_last(ctx, st);
     int rc = ensure_workspace(ctx, n, st);
     if (rc)
         return rc;
@@ -2942,6 +2991,10 @@ static int msg_stage(zmqg_ctx *ctx, size_t bytes)
     return 0;
 }
 
+// how long a per-message call polls its completion word before it
+// synchronises the stream instead
+static const int kMsgSpinUs = 200;
+
 // descriptors of the one message: sid, len, nonce / in_off, out_off, flags
 struct MsgDesc {
     uint32_t sid, len;
@@ -2953,16 +3006,19 @@ struct MsgDesc {
 
 // Wait for k_msg's completion word (the kernel's last write, system scope)
 // rather than for the stream: a poll of host memory sees it a few
-// microseconds before a stream synchronisation returns.  Bounded: after
-// 100 ms the stream is synchronised, which also reports a failed launch.
+// microseconds before a stream synchronisation returns.  The spin is bounded
+// by a few times the kernel's own latency (~5-7 us at <= 4 KiB, DESIGN.md
+// section 6): a call queued behind a long batch on another stream, or a
+// failed launch, falls back to the stream synchronisation instead of
+// holding a core (and the ctx's lock) in the loop.
 static int msg_wait(zmqg_ctx *ctx, const MsgDesc *h, hipStream_t st)
 {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
         if (__atomic_load_n(&h->done, __ATOMIC_ACQUIRE))
             return 0;
-        if ((spin & 1023u) == 1023u &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100))
+        if ((spin & 63u) == 63u &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kMsgSpinUs))
             break;
     }
     ZCHECK(ctx, hipStreamSynchronize(st));
@@ -2974,15 +3030,7 @@ static int msg_wait(zmqg_ctx *ctx, const MsgDesc *h, hipStream_t st)
 // session tables and the workspace, so own_stream waits for it first.
 static int msg_order(zmqg_ctx *ctx)
 {
-    hipStream_t last = ctx->last_stream;
-    if (last && last != ctx->own_stream) {
-        if (!ctx->order_ev)
-            ZCHECK(ctx, hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
-        ZCHECK(ctx, hipEventRecord(ctx->order_ev, last));
-        ZCHECK(ctx, hipStreamWaitEvent(ctx->own_stream, ctx->order_ev, 0));
-    }
-    ctx->last_stream = ctx->own_stream;
-    return 0;
+    return order_after_last(ctx, ctx->own_stream);
 }
 
 int zmqg_encode_msg(zmqg_ctx *ctx, uint32_t sid, uint64_t nonce, uint8_t flags, const uint8_t *in, uint32_t len,
@@ -3473,6 +3521,92 @@ int zmqg_fence_record(zmqg_ctx *ctx, void *stream, uint64_t *fence_out)
     return 0;
 }
 
+// The host function behind a notifying fence (zmqg_fence_record_notify): it
+// runs on a HIP runtime thread once the stream has passed the fence, marks
+// the fence reached and writes the caller's eventfd.  No HIP call in here.
+namespace {
+struct FenceNote {
+    zmqg_ctx *ctx;
+    uint64_t id;
+    int fd;
+};
+} // namespace
+
+static void fence_notify_fn(void *p)
+{
+    FenceNote *n = (FenceNote *) p;
+    zmqg_ctx *ctx = n->ctx;
+    {
+        std::lock_guard<std::mutex> lk(ctx->notify_mu);
+        ctx->notified.push_back(n->id);
+    }
+    const uint64_t one = 1;
+    ssize_t r;
+    do
+        r = write(n->fd, &one, sizeof one);
+    while (r < 0 && errno == EINTR);
+    delete n;
+    ctx->notify_pending.fetch_sub(1, std::memory_order_release); // (last touch of the ctx)
+}
+
+#ifndef ZMQG_BUILD_ID
+#define ZMQG_BUILD_ID "unstamped unstamped"
+#endif
+const char *zmqg_build_id(void)
+{
+    return ZMQG_BUILD_ID;
+}
+
+int zmqg_fence_record_notify(zmqg_ctx *ctx, void *stream, int fd, uint64_t *fence_out)
+{
+    if (!ctx || !fence_out || fd < 0)
+        return -EINVAL;
+    int rc = zmqg_fence_record(ctx, stream, fence_out);
+    if (rc)
+        return rc;
+    FenceNote *n = new FenceNote{ctx, *fence_out, fd};
+    ctx->notify_pending.fetch_add(1, std::memory_order_relaxed);
+    // after the fence's event in stream order: when it runs, the event has
+    // completed and so has every kernel of the batches before it
+    hipError_t e = hipLaunchHostFunc((hipStream_t) stream, fence_notify_fn, n);
+    if (e != hipSuccess) {
+        delete n;
+        ctx->notify_pending.fetch_sub(1, std::memory_order_release);
+        ZCHECK(ctx, e);
+    }
+    return 0;
+}
+
+int zmqg_notify_quiesce(zmqg_ctx *ctx)
+{
+    if (!ctx)
+        return -EINVAL;
+    while (ctx->notify_pending.load(std::memory_order_acquire) > 0)
+        sched_yield();
+    return 0;
+}
+
+// whether fence `id` has been marked reached by its notification (and
+// forget the marks of fences no longer pending)
+static bool fence_notified(zmqg_ctx *ctx, uint64_t id)
+{
+    std::lock_guard<std::mutex> lk(ctx->notify_mu);
+    bool hit = false;
+    for (size_t i = 0; i < ctx->notified.size();) {
+        const uint64_t v = ctx->notified[i];
+        bool pending = false;
+        for (auto &f : ctx->fences)
+            pending = pending || f.first == v;
+        if (v == id)
+            hit = true;
+        if (v == id || !pending)
+            ctx->notified.erase(ctx->notified.begin() + (long) i);
+        else
+            ++i;
+    }
+    return hit;
+}
+
 // 1 reached (and released), 0 pending, <0 error; `block` waits for it
 static int fence_check(zmqg_ctx *ctx, uint64_t fence, bool block)
 {
@@ -3485,10 +3619,12 @@ static int fence_check(zmqg_ctx *ctx, uint64_t fence, bool block)
         if (ctx->fences[i].first != fence)
             continue;
         hipEvent_t ev = ctx->fences[i].second;
-        hipError_t e = block ? hipEventSynchronize(ev) : hipEventQuery(ev);
-        if (e == hipErrorNotReady)
-            return 0;
-        ZCHECK(ctx, e);
+        if (!fence_notified(ctx, fence)) {
+            hipError_t e = block ? hipEventSynchronize(ev) : hipEventQuery(ev);
+            if (e == hipErrorNotReady)
+                return 0;
+            ZCHECK(ctx, e);
+        }
         ctx->fences.erase(ctx->fences.begin() + (long) i);
         ctx->fence_pool.push_back(ev);
         return 1;

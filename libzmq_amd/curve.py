@@ -104,7 +104,16 @@ _lib.zmqg_ctx_set_profiling.argtypes = [_P, ctypes.c_int]
 _lib.zmqg_ctx_get_profile.argtypes = [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
 _lib.zmqg_last_error.argtypes = [_P]
 _lib.zmqg_last_error.restype = ctypes.c_char_p
-assert _lib.zmqg_abi_version() == 4
+_lib.zmqg_fence_record_notify.argtypes = [_P, _P, ctypes.c_int, ctypes.POINTER(_U64)]
+_lib.zmqg_notify_quiesce.argtypes = [_P]
+_lib.zmqg_build_id.restype = ctypes.c_char_p
+assert _lib.zmqg_abi_version() == 5
+
+
+def build_id():
+    """(source id, commit) the loaded library was built from (zmqg_build_id)."""
+    sid, _, commit = _lib.zmqg_build_id().decode().partition(" ")
+    return sid, commit
 
 
 def lib():

@@ -35,8 +35,7 @@ curve_batcher_t::curve_batcher_t (zmqg_ctx *ctx_,
 curve_batcher_t::~curve_batcher_t ()
 {
     //  nothing may still be reading or writing a slot when it is freed
-    for (size_t i = 0; i < _flight.size (); ++i)
-        zmqg_fence_wait (_ctx, _flight[i]->fence);
+    wait_idle ();
     for (size_t i = 0; i < _slots.size (); ++i)
         if (_slots[i].base)
             zmqg_host_free (_ctx, _slots[i].base);
@@ -241,7 +240,10 @@ int curve_batcher_t::launch (slot_t *s)
                                    s->status, &o, _stream);
     }
     if (rc == 0)
-        rc = zmqg_fence_record (_ctx, _stream, &s->fence);
+        rc = _config.notify_fd >= 0
+               ? zmqg_fence_record_notify (_ctx, _stream, _config.notify_fd,
+                                           &s->fence)
+               : zmqg_fence_record (_ctx, _stream, &s->fence);
     if (rc != 0) {
         //  the slot's messages are lost with the device; keep the slot
         _free.push_back (s);
@@ -320,6 +322,19 @@ int curve_batcher_t::drain ()
         delivered += rc;
     }
     return delivered;
+}
+
+int curve_batcher_t::wait_idle ()
+{
+    int rc = 0;
+    for (size_t i = 0; i < _flight.size (); ++i) {
+        const int r = zmqg_fence_wait (_ctx, _flight[i]->fence);
+        if (r != 0 && rc == 0) {
+            errno = -r;
+            rc = -1;
+        }
+    }
+    return rc;
 }
 
 size_t curve_batcher_t::queued () const

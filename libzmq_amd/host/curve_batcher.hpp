@@ -83,8 +83,16 @@ class curve_batcher_t
         //  receive slots decoded with ZMQG_OPT_VERIFY_FIRST: the pinned slot
         //  never holds plaintext of a frame that fails (default on)
         bool verify_first;
+        //  >= 0: every launched slot's fence also writes this eventfd when
+        //  the stream reaches it (zmqg_fence_record_notify), so a poller
+        //  sleeping on it wakes for the completion.  -1: fences only.
+        int notify_fd;
         config_t () :
-            slot_msgs (8192), slot_bytes (8u << 20), slots (4), verify_first (true)
+            slot_msgs (8192),
+            slot_bytes (8u << 20),
+            slots (4),
+            verify_first (true),
+            notify_fd (-1)
         {
         }
     };
@@ -119,6 +127,9 @@ class curve_batcher_t
     int poll ();
     //  flush () and wait for and deliver everything.  Messages or -1.
     int drain ();
+
+    //  wait until no launched slot is still running (nothing delivered)
+    int wait_idle ();
 
     size_t queued () const;    //  messages submitted and not yet launched
     size_t in_flight () const; //  messages launched and not yet delivered

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_and_reports_abi_version():
     lib = ctypes.CDLL(LIB)
-    assert lib.zmqg_abi_version() == 4
+    assert lib.zmqg_abi_version() == 5
 
 
 def test_header_compiles_as_c():

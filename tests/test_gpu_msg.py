@@ -123,12 +123,15 @@ def test_decode_msg_in_place(torch_cuda, C):
         assert w[:size].tobytes() == pay
 
 
-def test_msg_calls_follow_a_batch_on_another_stream(torch_cuda, C):
+@pytest.mark.parametrize("where", ["side_stream", "null_stream"])
+def test_msg_calls_follow_a_batch_on_another_stream(torch_cuda, C, where):
     """A per-message call right after a batch call of the same ctx on another
     stream, with no synchronisation between them: the message kernel runs on
     the ctx's own stream after the batch (msg_order), so it sees the peer
     nonce the batch advanced -- the next nonce decodes, an old one is a
-    replay (src/curve_mechanism_base.cpp:98-106)."""
+    replay (src/curve_mechanism_base.cpp:98-106).  The batch stream is a
+    torch side stream, or the null stream (handle 0): the ctx's own stream
+    is non-blocking, so the null stream orders nothing by itself."""
     torch = torch_cuda
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(21)
@@ -152,10 +155,13 @@ def test_msg_calls_follow_a_batch_on_another_stream(torch_cuda, C):
     back = torch.zeros(n * P, dtype=torch.uint8, device=dev)
     fl = torch.zeros(n, dtype=torch.uint8, device=dev)
     st = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    s = torch.cuda.Stream()
-    with torch.cuda.stream(s):
-        dec.decode_batch(sid, w_off, wl, wire, in_off, back, fl, st, stream=s.cuda_stream)
-    got, gfl, gst = dec.decode_msg(0, nxt)  # no synchronisation with s before this call
+    if where == "side_stream":
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            dec.decode_batch(sid, w_off, wl, wire, in_off, back, fl, st, stream=s.cuda_stream)
+    else:
+        dec.decode_batch(sid, w_off, wl, wire, in_off, back, fl, st, stream=0)
+    got, gfl, gst = dec.decode_msg(0, nxt)  # no synchronisation with the batch stream before this call
     assert gst == 0 and got == b"after the batch" and gfl == 1
     _, _, gst = dec.decode_msg(0, old)
     assert gst == C.ERR_INVALID_SEQUENCE

@@ -1,8 +1,8 @@
 #!/bin/bash
 # k_body diagnostics: kernel timings at config-5
 # frame size (128 x 16 MiB, 8 sessions) for the default build and the timing
-# ablations (build/libzmqg_body_ab<V>.so = -DZMQG_ABLATE=V; outputs garbage),
-# per-tile phase stamps (build/libzmqg_curve_stamps.so, tools/stamps.py), a
+# ablations (tools/bin/libzmqg_body_ab<V>.so = -DZMQG_ABLATE=V; outputs garbage),
+# per-tile phase stamps (tools/bin/libzmqg_curve_stamps.so, tools/stamps.py), a
 # rocprofv3 kernel-stats pass over bench.py's configs 3/4/5, and one PMC pass
 # of instruction counts and wave-cycle shares of k_body.
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -11,10 +11,10 @@ mkdir -p gpurun_out
 SHAPE="--msgs ${MSGS:-128} --size ${SIZE:-16777216} --sessions ${SESS:-8}"
 timeout -k 10 180 python tools/kbench.py --iters 5 $SHAPE --tag body || exit 1
 for v in ${ABL:-2 3 4 5}; do
-  [ -f build/libzmqg_body_ab$v.so ] || continue
-  ZMQG_CURVE_LIB=$PWD/build/libzmqg_body_ab$v.so timeout -k 10 180 python tools/kbench.py --iters 5 $SHAPE --tag body_ab$v || exit 1
+  [ -f tools/bin/libzmqg_body_ab$v.so ] || continue
+  ZMQG_CURVE_LIB=$PWD/tools/bin/libzmqg_body_ab$v.so timeout -k 10 180 python tools/kbench.py --iters 5 $SHAPE --tag body_ab$v || exit 1
 done
-if [ -f build/libzmqg_curve_stamps.so ]; then
+if [ -f tools/bin/libzmqg_curve_stamps.so ]; then
   timeout -k 10 180 python tools/stamps.py $SHAPE --tag stamps || exit 1
 fi
 [ -n "$NOPROF" ] && exit 0

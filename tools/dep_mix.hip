@@ -1,7 +1,7 @@
 // Dependent VOP2/VOP3 chains on gfx950 (why a Salsa20 block costs more than
 // the sum of its instructions' independent issue costs): C chains of
 // add -> alignbit -> xor steps (each step's add reads the previous xor).
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/dep_mix tools/dep_mix.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/dep_mix tools/dep_mix.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -3,7 +3,7 @@
 // window (64 B), with D windows of loads in flight, in two access shapes:
 //   LANE  lane = frame, each lane loads its own 4 x 16 B per window
 //   COOP  4 lanes per frame-window (16 frames per instruction)
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/framecopy tools/framecopy.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/framecopy tools/framecopy.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -1,6 +1,6 @@
 // Frame kernel (libzmq_amd/csrc/curve_frames.hpp) against the library's
 // head/body path: bit-exactness and timing at G = 1, 2, 4 lanes per frame.
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/frames_bench tools/frames_bench.hip -Llibzmq_amd -lzmqg_curve
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/frames_bench tools/frames_bench.hip -Llibzmq_amd -lzmqg_curve
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -4,7 +4,7 @@
 // 9 steps per lane.  F = feature bits: 1 input loads (a step ahead) + XOR,
 // 2 input byte shift, 4 output stores (aligned, no shift), 8 output shift,
 // 16 Poly1305 (parallel form, as curve_frames.hpp), 32 s_setprio schedule.
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/frames_proto tools/frames_proto.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/frames_proto tools/frames_proto.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

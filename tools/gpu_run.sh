@@ -1,0 +1,122 @@
+#!/bin/bash
+# One entry point for the GPU-box runs behind DESIGN.md and profiles/
+# (replaces round 4's eighteen one-off tools/gpu_r4_*.sh scripts).
+#
+#   gpurun -- 'bash tools/gpu_run.sh MODE [ARGS]'
+#
+# MODE
+#   suite            the whole -m gpu suite in one process, then smoke()
+#   bench            the bench line with the driver's arguments (K=20, W=5)
+#   prof             rocprofv3 --kernel-trace --stats of the config-2-only bench
+#                    (profiles/<tag>_config2_kernel_stats.csv), then of the full
+#                    bench (all configs) -- ARGS: tag (default rNN)
+#   pmc              PMC passes of the config-2 bench for profiles/pmc_*_config2.json
+#                    (tools/pmc_profiles.sh; summarise with tools/pmc_profiles.py)
+#   ab LIB [SHAPE]   config-2 (or SHAPE = kbench args) frame kernels of library
+#                    LIB against the tree's, alternating, three rounds
+#   benchab LIB      the bench line of LIB against the tree's, alternating
+#   zmtp             tests/test_zmtp.py, tools/zmtp_bench.py twice, a kernel trace
+#   msg              per-message path: its tests, tools/bin/msg_kernel_bench
+#                    (per call), tools/bin/msg_latency (round trips)
+#   cfg4             config 4 as the bench runs it, each frame-kernel variant forced
+#   twowave          one-lane kernels at one and two waves per SIMD over 64 MiB
+#   engine           the host-adapter tests (batcher, engine hook with epoll)
+# Every GPU step runs under its own time limit and the script stops at the
+# first failure.
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+MODE=${1:-suite}
+shift
+PYTEST="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
+kb() { timeout -k 10 180 python -u tools/kbench.py "$@"; }
+
+case $MODE in
+suite)
+  timeout -k 10 1000 $PYTEST tests -m gpu > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -3
+  [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_gpu.log | head -80; exit 1; }
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+  ;;
+bench)
+  timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err \
+    || { tail -20 gpurun_out/bench.err; exit 1; }
+  tail -1 gpurun_out/bench.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['pmc_files'], {k: round(v['value'],1) for k,v in d.get('configs',{}).items()})"
+  ;;
+prof)
+  TAG=${1:-rNN}
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $PWD/gpurun_out/prof_c2 -o c2 --output-format csv -- \
+      python3 bench.py --steps 20 --warmup 5 --no-configs --no-host-staged --no-cpu-baseline \
+      > gpurun_out/prof_c2.json 2> gpurun_out/prof_c2.err || { tail -20 gpurun_out/prof_c2.err; exit 1; }
+  tail -1 gpurun_out/prof_c2.json
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $PWD/gpurun_out/prof_all -o all --output-format csv -- \
+      python3 bench.py --steps 20 --warmup 5 --no-host-staged --no-cpu-baseline \
+      > gpurun_out/prof_all.json 2> gpurun_out/prof_all.err || { tail -20 gpurun_out/prof_all.err; exit 1; }
+  find gpurun_out/prof_c2 gpurun_out/prof_all -name "*kernel_stats.csv"
+  ;;
+pmc)
+  bash tools/pmc_profiles.sh || exit 1
+  ;;
+ab)
+  A=$1; shift
+  for r in 1 2 3; do
+    for lib in $A libzmq_amd/libzmqg_curve.so; do
+      ZMQG_CURVE_LIB=$PWD/$lib kb --tag $lib "$@" > gpurun_out/ab.log 2>&1 || { tail -20 gpurun_out/ab.log; exit 1; }
+      tail -1 gpurun_out/ab.log
+    done
+  done
+  ;;
+benchab)
+  A=$1
+  for r in 1 2; do
+    for lib in $A libzmq_amd/libzmqg_curve.so; do
+      ZMQG_CURVE_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline \
+          --no-host-staged --no-configs > gpurun_out/benchab.json 2> gpurun_out/benchab.err \
+          || { tail -20 gpurun_out/benchab.err; exit 1; }
+      tail -1 gpurun_out/benchab.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$lib', round(d['value'],1), round(d['ms_per_step']*1000,1), round(d['roofline']['avg_launch_us'],1), round(d['roofline']['encode_main_avg_us'],1))"
+    done
+  done
+  ;;
+zmtp)
+  timeout -k 10 300 $PYTEST tests/test_zmtp.py -m gpu > gpurun_out/pytest_zmtp.log 2>&1 \
+    || { tail -40 gpurun_out/pytest_zmtp.log; exit 1; }
+  tail -1 gpurun_out/pytest_zmtp.log
+  for r in 1 2; do
+    timeout -k 10 180 python -u tools/zmtp_bench.py || exit 1
+  done
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $PWD/gpurun_out/zprof -o run --output-format csv -- \
+      python -u tools/zmtp_bench.py > gpurun_out/zprof.log 2>&1 || { tail -20 gpurun_out/zprof.log; exit 1; }
+  ;;
+msg)
+  timeout -k 10 300 $PYTEST tests/test_gpu_msg.py tests/test_host_adapter.py -m gpu > gpurun_out/pytest_msg.log 2>&1 \
+    || { tail -30 gpurun_out/pytest_msg.log; exit 1; }
+  tail -1 gpurun_out/pytest_msg.log
+  LD_LIBRARY_PATH=$PWD/libzmq_amd:$LD_LIBRARY_PATH timeout -k 10 120 ./tools/bin/msg_kernel_bench tree || exit 1
+  timeout -k 10 120 ./tools/bin/msg_latency > gpurun_out/msg_latency.json 2>&1 || exit 1
+  grep '^{' gpurun_out/msg_latency.json
+  ;;
+cfg4)
+  for r in 1 2; do
+    for g in default 0 8; do
+      if [ $g = default ]; then unset ZMQG_FRAMES_G; else export ZMQG_FRAMES_G=$g; fi
+      timeout -k 10 300 python bench.py --steps 5 --warmup 2 --configs 4 --no-cpu-baseline --no-host-staged 2>/dev/null \
+        | python3 -c "import sys,json; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); c=d['configs']['config4']; print('G=$g', 'config4', round(c['value'],1), 'GiB/s', round(c['ms_per_step'],3), 'ms/step')" || exit 1
+    done
+  done
+  ;;
+twowave)
+  for r in 1 2; do
+    for g in 0 8; do
+      ZMQG_FRAMES_G=$g kb --iters 30 --msgs 65536 --size 1024 --tag G$g-65536x1024 || exit 1
+      ZMQG_FRAMES_G=$g kb --iters 30 --msgs 131072 --size 512 --tag G$g-131072x512 || exit 1
+    done
+  done
+  ;;
+engine)
+  timeout -k 10 600 $PYTEST tests/test_host_adapter.py tests/test_gpu_notify.py -m gpu > gpurun_out/pytest_engine.log 2>&1
+  rc=$?; tail -3 gpurun_out/pytest_engine.log; [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_engine.log | head -60; exit 1; }
+  ;;
+*)
+  echo "unknown mode $MODE"; exit 2
+  ;;
+esac

@@ -1,7 +1,7 @@
 // Round 4: the floor under a per-message call -- one kernel launch that
 // only sets a completion word in mapped host memory, the host polling it
 // (the shape of zmqg_encode_msg's wait), against hipStreamSynchronize.
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/launch_floor tools/launch_floor.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/launch_floor tools/launch_floor.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

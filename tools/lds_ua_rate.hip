@@ -1,7 +1,7 @@
 // Unaligned LDS access on gfx950: correctness of ds_read/ds_write b32/b128 at
 // byte offsets 0..3 (and 4..15 for b128), and cycles per wave-instruction
 // (one wave per SIMD, 16 independent accesses per iteration), aligned vs not.
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/lds_ua_rate tools/lds_ua_rate.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/lds_ua_rate tools/lds_ua_rate.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -2,7 +2,7 @@
 // diagnostic builds with parts of k_msg ablated can be timed; run under
 // rocprofv3 --kernel-trace --stats for the kernel's own duration).
 // Build: g++ -O2 -std=c++11 tools/msg_kernel_bench.cpp -Llibzmq_amd -lzmqg_curve
-//        -Wl,-rpath,$PWD/libzmq_amd -o build/msg_kernel_bench   (ZMQG_CURVE_SO: none; link a build)
+//        -Wl,-rpath,$PWD/libzmq_amd -o tools/bin/msg_kernel_bench   (ZMQG_CURVE_SO: none; link a build)
 #include "../include/zmqg_curve.h"
 
 #include <chrono>

@@ -10,7 +10,7 @@
 // Prints us per encode+decode round trip by payload size.
 // Build: g++ -O2 -std=c++11 -Ilibzmq_amd/host tools/msg_latency.cpp
 //        libzmq_amd/host/curve_encoding_gpu.cpp -Llibzmq_amd -lzmqg_curve
-//        -Wl,-rpath,$PWD/libzmq_amd -o build/msg_latency
+//        -Wl,-rpath,$PWD/libzmq_amd -o tools/bin/msg_latency
 #include "curve_encoding_gpu.hpp"
 
 #include <chrono>

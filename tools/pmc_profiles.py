@@ -30,6 +30,20 @@ def pick(acc, pat, counter):
     raise KeyError(pat)
 
 
+def build_of(log):
+    """the bench line's build (zmqg_build_id of the library the pass loaded)"""
+    for line in reversed(open(log).read().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)["build"]
+    raise ValueError(f"no bench line in {log}")
+
+
+builds = {build_of(f)["source_id"]: build_of(f) for f in
+          glob.glob(f"{root}/pmcv/run.log") + glob.glob(f"{root}/pmcs/run.log") + glob.glob(f"{root}/pmct/fetch.log")
+          + glob.glob(f"{root}/pmct/write.log")}
+assert len(builds) == 1, f"PMC passes of different builds: {sorted(builds)}"
+build = next(iter(builds.values()))
+
 valu = json.load(open(f"{root}/pmcv/summary.json"))
 try:
     stall = json.load(open(f"{root}/pmcs/summary.json"))
@@ -72,6 +86,7 @@ for dec in (True, False):
         out_t["encode"] = t
         out_v["encode"] = vv
 out_t.update({
+    "source_id": build["source_id"], "commit": build["commit"],
     "workload": "config2: 65536 x 1024 B frames, one session, one lane per frame (1024 waves, 1 per SIMD)",
     "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace) of python bench.py "
               "--eager --steps 3 --warmup 1 (tools/pmc_traffic.sh via tools/pmc_profiles.sh); calibration: the same "
@@ -83,6 +98,7 @@ out_t.update({
                         "the bytes moved (partial-line writes), the same kind of amplification as the frame kernel."
                         % (cal_f, moved_kib, scale, cal_w / moved_kib)})
 out_v.update({
+    "source_id": build["source_id"], "commit": build["commit"],
     "workload": out_t["workload"],
     "source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES "
               "--kernel-trace of python bench.py --eager --steps 3 --warmup 1 (tools/pmc_valu_bench.sh)",

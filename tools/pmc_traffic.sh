@@ -13,6 +13,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $PWD/$O/$t -o pmc -- \
       python bench.py --eager --steps 3 --warmup 1 --no-cpu-baseline --no-host-staged --no-configs > $O/$t.log 2>&1 || { echo "bench pass $c failed"; exit 1; }
   timeout -s KILL 60 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $PWD/$O/${t}_cal -o pmc -- \
-      ./build/framecopy > $O/${t}_cal.log 2>&1 || { echo "calibration pass $c failed"; exit 1; }
+      ./tools/bin/framecopy > $O/${t}_cal.log 2>&1 || { echo "calibration pass $c failed"; exit 1; }
 done
 echo done

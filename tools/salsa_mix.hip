@@ -4,7 +4,7 @@
 // tools/valu_rates.hip).  VOP3-encoded ops (v_alignbit_b32, v_bitop3_b32,
 // v_lshl_or_b32) issue at about half the rate of VOP2 ops (v_add_u32,
 // v_xor_b32, shifts): profiles/valu_rates_r02.md.
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/salsa_mix tools/salsa_mix.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/salsa_mix tools/salsa_mix.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

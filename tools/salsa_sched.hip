@@ -5,9 +5,9 @@
 // issue faster than the compiler's order once two waves share a SIMD
 // (profiles/valu_rates_r02.md: an independent 2 VOP2 : 1 VOP3 mix issues at
 // ~2.9 cycles per instruction at two waves, the compiler's Salsa20 block at ~4).
-// Build: python3 tools/gen_salsa_sched.py build/salsa_sched_gen.hpp &&
-//        python3 tools/gen_salsa_asm.py build/curve_salsa_asm.hpp &&
-//        hipcc -O3 --offload-arch=gfx950 -Ibuild -o build/salsa_sched tools/salsa_sched.hip
+// Build: python3 tools/gen_salsa_sched.py tools/bin/salsa_sched_gen.hpp &&
+//        python3 tools/gen_salsa_asm.py tools/bin/curve_salsa_asm.hpp &&
+//        hipcc -O3 --offload-arch=gfx950 -Itools/bin -o tools/bin/salsa_sched tools/salsa_sched.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

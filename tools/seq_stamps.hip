@@ -4,7 +4,7 @@
 // wait for step t's input words (24+t), after the loop (60), at the end
 // (61); for steps 1..7 also after the input words are in (44+t), before the
 // stores (52+t) and after them (36+t).  Config-2 shape: 65,536 frames of 1 KiB, encode then decode.
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DZMQG_SEQ_STAMPS=1 -o build/seq_stamps tools/seq_stamps.hip
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DZMQG_SEQ_STAMPS=1 -o tools/bin/seq_stamps tools/seq_stamps.hip
 // (add -DSTAMP_LDS=1 for k_frames_lds: slots 3+t step start, 44+t after the
 // wait, 52+t after the DMA and store issue, 24+t after keystream and MAC,
 // 36+t after the ring write)

@@ -11,7 +11,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-lib = os.path.join(ROOT, "build", "libzmqg_curve_stamps.so")
+lib = os.path.join(ROOT, "tools", "bin", "libzmqg_curve_stamps.so")
 os.environ["ZMQG_CURVE_LIB"] = lib
 sys.argv = [sys.argv[0], "--iters", "1"] + sys.argv[1:]
 sys.path.insert(0, ROOT)

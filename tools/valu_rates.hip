@@ -11,7 +11,7 @@
 // MHz reference); per SIMD instruction count = k x iters x instructions per
 // iteration.  Output: one JSON object per line (tools/valu_rates.py makes
 // the table under profiles/).
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/valu_rates tools/valu_rates.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/valu_rates tools/valu_rates.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -4,7 +4,7 @@
 // strided 1,057 bytes apart (the config-2 frame stride), 4-byte aligned
 // (misaligned to 16) or 16-byte aligned.  Cycles per instruction per wave
 // from s_memtime around bursts of 8 instructions (no wait inside the burst).
-// Build: hipcc -O3 --offload-arch=gfx950 -o build/vmem_issue tools/vmem_issue.hip
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/bin/vmem_issue tools/vmem_issue.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -84,11 +84,11 @@ def main():
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    def d_zmtp():
+    def d_zmtp(maxmsg=-1):
         d.set_peer_nonce(0, 2)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        r = d.decode_zmtp(0, framed, total, -1, n, d_foff, d_flen, d_poff, zback, fl, st)
+        r = d.decode_zmtp(0, framed, total, maxmsg, n, d_foff, d_flen, d_poff, zback, fl, st)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         assert r["frames"] == n and r["consumed"] == total and r["error"] == 0
@@ -105,6 +105,15 @@ def main():
     idx = d_poff[:, None] + torch.arange(P, device=dev)[None, :]
     assert int((st != 0).sum()) == 0 and torch.equal(zback[idx].reshape(-1), pay)
     print(f"decode_batch {tb:8.1f} us   decode_zmtp {tzd:8.1f} us  (parse + decode, synchronous)")
+    # the engine's ZMQ_MAXMSGSIZE (options.maxmsgsize, checked by the v2
+    # decoder against each frame's size, src/v2_decoder.cpp:74-84) at the
+    # frames' own size: every frame is known to fit the frame kernel, so the
+    # large-frame launches are skipped
+    zback.zero_()
+    d_zmtp(W)
+    tzm = min(d_zmtp(W) for _ in range(5)) * 1e6
+    assert int((st != 0).sum()) == 0 and torch.equal(zback[idx].reshape(-1), pay)
+    print(f"decode_zmtp_maxmsgsize {tzm:8.1f} us  (max_msg_size = {W})")
 
 
 if __name__ == "__main__":
