@@ -1,0 +1,212 @@
+// CURVE PUSH/PULL over TCP between two libzmq builds (config 1's plumbing,
+// BASELINE.json configs[0]): the stock reference library, whose MESSAGE
+// codec is libsodium's, and the same library with the GPU codec swapped in
+// (tests/host/build_libzmq.sh).  Written against the public zmq.h API only,
+// in the shape of the reference's perf/local_thr.cpp (PULL, binds,
+// receives) and perf/remote_thr.cpp (PUSH, connects, sends) with CURVE set
+// up as tests/test_security_curve.cpp does (server: ZMQ_CURVE_SERVER and its
+// secret key; client: the server's public key and its own key pair), using
+// the test key pairs of doc/zmq_curve.adoc.
+//
+//   interop pull <endpoint> <ack_endpoint> <messages> <seed> <heartbeat_ivl_ms>
+//   interop push <endpoint> <ack_endpoint> <messages> <seed> <heartbeat_ivl_ms>
+//
+// Once everything has arrived the PULL side answers on a second CURVE
+// connection the other way (the PUSH process binds a CURVE-server PULL on
+// ack_endpoint, the PULL process connects a client PUSH), so the sender
+// closes only after delivery -- and each process runs both a CURVE client
+// and a CURVE server.  (Closing right after the last send lost the tail of
+// the stream with heartbeats on, with the stock library on both sides.)
+//
+// Message i of the plan (both sides derive it from the seed): one part of
+// 1,024 bytes, except every 1,000th message from offset 1 .. 4 (0 B, 33 B,
+// 64 KiB, 64 B) and every 50th (offset 7) is three parts (MORE) of 1 KiB,
+// 100 B and 0 B; each byte comes from a splitmix64 stream keyed by (seed,
+// message, part).  The receiver checks every part byte for byte, its size
+// and its MORE flag, and prints "OK <messages> <parts> <msgs/s> <MB/s>".
+// ZMTP heartbeats (ZMQ_HEARTBEAT_IVL) run on both sides, so PING/PONG
+// commands go through the codec too (src/zmtp_engine.cpp:463, 479).
+#include <zmq.h>
+
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <vector>
+
+static const char server_public[] = "rq:rM>}U?@Lns47E1%kR.o@n%FcmmsL/@{H8]yf7";
+static const char server_secret[] = "JTKVSB%%)wK0E.X)V>+}o?pNmC{O&4W4b!Ni{Lh6";
+static const char client_public[] = "Yne@$w-vo<fVvi]a<NY6T1ed:M$fCG*[IaLV{hID";
+static const char client_secret[] = "D:)Q[IlAW!ahhC2ac:9*A}h:p?([4%wOTJ%JR%cs";
+
+#define CHECK(c)                                                               \
+    do {                                                                       \
+        if (!(c)) {                                                            \
+            fprintf (stderr, "%s:%d: check failed: %s (errno %d: %s)\n",       \
+                     __FILE__, __LINE__, #c, zmq_errno (),                      \
+                     zmq_strerror (zmq_errno ()));                              \
+            exit (1);                                                          \
+        }                                                                      \
+    } while (0)
+
+static uint64_t splitmix (uint64_t &s_)
+{
+    uint64_t z = (s_ += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+//  the parts of message i
+static void plan (uint64_t seed_, uint64_t i_, std::vector<std::vector<uint8_t> > &parts_)
+{
+    static const size_t special[] = {0, 33, 65536, 64};
+    std::vector<size_t> sizes;
+    if (i_ % 1000 >= 1 && i_ % 1000 <= 4)
+        sizes.push_back (special[i_ % 1000 - 1]);
+    else if (i_ % 50 == 7) {
+        sizes.push_back (1024);
+        sizes.push_back (100);
+        sizes.push_back (0);
+    } else
+        sizes.push_back (1024);
+    parts_.resize (sizes.size ());
+    for (size_t p = 0; p < sizes.size (); ++p) {
+        uint64_t s = seed_ * 0x100000001b3ull + i_ * 8 + p;
+        parts_[p].resize (sizes[p]);
+        for (size_t k = 0; k < sizes[p]; k += 8) {
+            const uint64_t v = splitmix (s);
+            for (size_t b = 0; b < 8 && k + b < sizes[p]; ++b)
+                parts_[p][k + b] = (uint8_t) (v >> (8 * b));
+        }
+    }
+}
+
+static double now_s ()
+{
+    timespec t;
+    clock_gettime (CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+static void setup_heartbeats (void *s_, int ivl_)
+{
+    if (ivl_ <= 0)
+        return;
+    const int timeout = 10000, ttl = 10000;
+    CHECK (zmq_setsockopt (s_, ZMQ_HEARTBEAT_IVL, &ivl_, sizeof ivl_) == 0);
+    CHECK (zmq_setsockopt (s_, ZMQ_HEARTBEAT_TIMEOUT, &timeout, sizeof timeout) == 0);
+    CHECK (zmq_setsockopt (s_, ZMQ_HEARTBEAT_TTL, &ttl, sizeof ttl) == 0);
+}
+
+int main (int argc, char **argv)
+{
+    if (argc != 7) {
+        fprintf (stderr, "usage: %s pull|push <endpoint> <ack_endpoint> <messages> <seed> <heartbeat_ivl_ms>\n",
+                 argv[0]);
+        return 2;
+    }
+    const bool pull = strcmp (argv[1], "pull") == 0;
+    const char *endpoint = argv[2];
+    const char *ack_endpoint = argv[3];
+    const uint64_t n = strtoull (argv[4], NULL, 10);
+    const uint64_t seed = strtoull (argv[5], NULL, 10);
+    const int ivl = atoi (argv[6]);
+    CHECK (zmq_has ("curve"));
+
+    void *ctx = zmq_ctx_new ();
+    CHECK (ctx);
+    std::vector<std::vector<uint8_t> > parts;
+    if (pull) {
+        //  perf/local_thr.cpp, as the CURVE server (tests/test_security_curve.cpp)
+        void *s = zmq_socket (ctx, ZMQ_PULL);
+        CHECK (s);
+        const int one = 1, rcvtimeo = 30000;
+        CHECK (zmq_setsockopt (s, ZMQ_CURVE_SERVER, &one, sizeof one) == 0);
+        CHECK (zmq_setsockopt (s, ZMQ_CURVE_SECRETKEY, server_secret, 40) == 0);
+        CHECK (zmq_setsockopt (s, ZMQ_RCVTIMEO, &rcvtimeo, sizeof rcvtimeo) == 0);
+        setup_heartbeats (s, ivl);
+        CHECK (zmq_bind (s, endpoint) == 0);
+        printf ("READY\n");
+        fflush (stdout);
+        zmq_msg_t m;
+        CHECK (zmq_msg_init (&m) == 0);
+        uint64_t frames = 0, bytes = 0;
+        double t0 = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            plan (seed, i, parts);
+            for (size_t p = 0; p < parts.size (); ++p) {
+                const int rc = zmq_msg_recv (&m, s, 0);
+                if (rc < 0) {
+                    fprintf (stderr, "FAIL: receive of message %llu part %zu: %s\n", (unsigned long long) i, p,
+                             zmq_strerror (zmq_errno ()));
+                    return 1;
+                }
+                if (i == 0 && p == 0)
+                    t0 = now_s ();
+                const bool more = zmq_msg_more (&m) != 0;
+                if ((size_t) rc != parts[p].size () || more != (p + 1 < parts.size ())
+                    || (rc && memcmp (zmq_msg_data (&m), &parts[p][0], rc) != 0)) {
+                    fprintf (stderr, "FAIL: message %llu part %zu: size %d (want %zu), more %d\n",
+                             (unsigned long long) i, p, rc, parts[p].size (), (int) more);
+                    return 1;
+                }
+                ++frames;
+                bytes += rc;
+            }
+        }
+        const double dt = now_s () - t0;
+        CHECK (zmq_msg_close (&m) == 0);
+        //  the acknowledgement, as a CURVE client of the sender's process
+        void *a = zmq_socket (ctx, ZMQ_PUSH);
+        CHECK (a);
+        CHECK (zmq_setsockopt (a, ZMQ_CURVE_SERVERKEY, server_public, 40) == 0);
+        CHECK (zmq_setsockopt (a, ZMQ_CURVE_PUBLICKEY, client_public, 40) == 0);
+        CHECK (zmq_setsockopt (a, ZMQ_CURVE_SECRETKEY, client_secret, 40) == 0);
+        CHECK (zmq_connect (a, ack_endpoint) == 0);
+        CHECK (zmq_send (a, "DONE", 4, 0) == 4);
+        CHECK (zmq_close (a) == 0);
+        CHECK (zmq_close (s) == 0);
+        CHECK (zmq_ctx_term (ctx) == 0);
+        printf ("OK %llu %llu %.0f %.1f\n", (unsigned long long) n, (unsigned long long) frames,
+                dt > 0 ? (n - 1) / dt : 0.0, dt > 0 ? bytes / dt / 1e6 : 0.0);
+        return 0;
+    }
+    //  the acknowledgement's receiver, as a CURVE server
+    void *a = zmq_socket (ctx, ZMQ_PULL);
+    CHECK (a);
+    const int one = 1, acktimeo = 60000;
+    CHECK (zmq_setsockopt (a, ZMQ_CURVE_SERVER, &one, sizeof one) == 0);
+    CHECK (zmq_setsockopt (a, ZMQ_CURVE_SECRETKEY, server_secret, 40) == 0);
+    CHECK (zmq_setsockopt (a, ZMQ_RCVTIMEO, &acktimeo, sizeof acktimeo) == 0);
+    CHECK (zmq_bind (a, ack_endpoint) == 0);
+    //  perf/remote_thr.cpp, as the CURVE client
+    void *s = zmq_socket (ctx, ZMQ_PUSH);
+    CHECK (s);
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_SERVERKEY, server_public, 40) == 0);
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_PUBLICKEY, client_public, 40) == 0);
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_SECRETKEY, client_secret, 40) == 0);
+    setup_heartbeats (s, ivl);
+    CHECK (zmq_connect (s, endpoint) == 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        plan (seed, i, parts);
+        for (size_t p = 0; p < parts.size (); ++p)
+            CHECK (zmq_send (s, parts[p].empty () ? NULL : &parts[p][0], parts[p].size (),
+                             p + 1 < parts.size () ? ZMQ_SNDMORE : 0)
+                   == (int) parts[p].size ());
+    }
+    char ack[8];
+    const int rc = zmq_recv (a, ack, sizeof ack, 0);
+    if (rc != 4 || memcmp (ack, "DONE", 4) != 0) {
+        fprintf (stderr, "FAIL: no acknowledgement (%d)\n", rc);
+        return 1;
+    }
+    CHECK (zmq_close (a) == 0);
+    CHECK (zmq_close (s) == 0);
+    CHECK (zmq_ctx_term (ctx) == 0);
+    printf ("SENT %llu ACKED\n", (unsigned long long) n);
+    return 0;
+}

@@ -1,0 +1,90 @@
+"""Config 1's plumbing (BASELINE.json configs[0]): CURVE PUSH/PULL over
+tcp://127.0.0.1 between two builds of the reference libzmq -- the stock one
+(libsodium codec) and the one with INTEGRATION.md section 2 applied
+(tests/host/libzmq_zmqg.patch: curve_encoding_t swapped for the GPU codec,
+the stream engine, I/O threads, handshake and sockets untouched).  Built by
+tests/host/build_libzmq.sh (run by __graft_entry__.build()); the test
+program is tests/host/test_curve_interop.cpp, shaped like the reference's
+perf/local_thr.cpp / perf/remote_thr.cpp with CURVE set up as
+tests/test_security_curve.cpp does.
+
+Each run sends 100,000 messages (1 KiB, plus 0 B, 33 B, 64 B and 64 KiB ones
+and three-part MORE messages) with ZMTP heartbeats every 5 ms on both
+sides (PING/PONG through the codec, src/zmtp_engine.cpp:463, 479); the
+receiver checks every part byte for byte, its size and its MORE flag, then
+acknowledges over a second CURVE connection the other way.  This is
+interop evidence between the two codecs on real sockets, not an oracle pin.
+
+CPU: the stock pair (checks the harness).  GPU: GPU-codec server with a
+stock client, the reverse, and GPU on both sides."""
+import os
+import socket
+import subprocess
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "host", "_ref", "libzmq")
+N = 100000
+
+
+def _exe(kind):
+    p = os.path.join(BIN, "interop_" + kind)
+    if not os.path.exists(p):
+        pytest.skip("interop build absent (tests/host/build_libzmq.sh needs /root/reference and libsodium)")
+    return p
+
+
+def _ports():
+    socks = []
+    for _ in range(2):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+    ports = [s.getsockname()[1] for s in socks]
+    for s in socks:
+        s.close()
+    return ports
+
+
+def run_pair(server_kind, client_kind, n=N, seed=11, heartbeat_ms=5):
+    """PULL (CURVE server) built as server_kind, PUSH (CURVE client) as
+    client_kind; returns the receiver's line: OK n parts msgs/s MB/s."""
+    srv, cli = _exe(server_kind), _exe(client_kind)
+    p, q = _ports()
+    ep, ack = f"tcp://127.0.0.1:{p}", f"tcp://127.0.0.1:{q}"
+    args = [ep, ack, str(n), str(seed), str(heartbeat_ms)]
+    pull = subprocess.Popen([srv, "pull"] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        assert pull.stdout.readline().strip() == "READY"
+        push = subprocess.run([cli, "push"] + args, capture_output=True, text=True, timeout=240)
+        out, err = pull.communicate(timeout=60)
+    finally:
+        if pull.poll() is None:
+            pull.kill()
+            pull.wait()
+    assert push.returncode == 0, push.stderr + push.stdout
+    assert push.stdout.strip() == f"SENT {n} ACKED"
+    assert pull.returncode == 0, err + out
+    line = out.strip().splitlines()[-1]
+    f = line.split()
+    assert f[0] == "OK" and int(f[1]) == n, line
+    return {"server": server_kind, "client": client_kind, "messages": n, "parts": int(f[2]),
+            "msgs_per_s": float(f[3]), "MB_per_s": float(f[4])}
+
+
+def test_stock_pair_delivers_everything():
+    r = run_pair("stock", "stock")
+    print(r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("server,client", [("zmqg", "stock"), ("stock", "zmqg"), ("zmqg", "zmqg")])
+def test_gpu_codec_interoperates_with_stock(server, client):
+    """Every message arrives byte-exact across the two codecs, in both
+    directions of the CURVE roles, with heartbeats on."""
+    t0 = time.time()
+    r = run_pair(server, client)
+    r["wall_s"] = time.time() - t0
+    print(r)
