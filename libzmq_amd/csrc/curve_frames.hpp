@@ -353,6 +353,10 @@ struct FrameCtl {
     unsigned long long *nonce_ctr; // encode, one session, ZMQG_OPT_NONCE_AUTO: the session's send
                                    // counter; frame i takes *nonce_ctr + i, the last workgroup adds n
     uint64_t out_limit;  // (out_check) the caller's out_bytes: the staging area's extent
+    // k_frames_split: workgroups [0, split_wg) run the one-lane-per-frame body
+    // on frames [0, split_n) (split_n = split_wg x kFramesBS), the rest run the
+    // G-lanes-per-frame body on frames [split_n, n); 0 in every other launch
+    uint32_t split_wg, split_n;
 };
 
 // msg_t flags a received ZMTP frame adds to its decoded message: the
@@ -573,15 +577,23 @@ struct NoBigFrames {
 // an entry in this call's big-frame list).
 // zs: the context's call state (see ZState); decode with rp.lb_flag set
 // applies the one-session replay rule in this kernel.
+#define ZMQG_FRAMES_PARAMS                                                                                    \
+    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce,                             \
+        const uint8_t *__restrict__ flags, const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, \
+        const uint8_t *__restrict__ in, const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,          \
+        const DevSession *__restrict__ sessions, uint32_t max_sessions, uint32_t max_stream,                      \
+        uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out, ReplayOut rp, BigOp big,               \
+        ZState *__restrict__ zs, FrameCtl ctl
+#define ZMQG_FRAMES_ARGS                                                                                      \
+    n, sid, nonce, flags, in_off, len, in, out_off, out, sessions, max_sessions, max_stream, flags_out,           \
+        status_out, rp, big, zs, ctl
+
+// (the body of k_frames<G>; in a k_frames_split launch its workgroups are
+// those from ctl.split_wg on and its frames those from ctl.split_n on)
 template <bool DEC, int G, class BigOp>
-__global__ __launch_bounds__(kFramesBS) void k_frames(
-    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
-    const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
-    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
-    uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
-    ReplayOut rp, BigOp big, ZState *__restrict__ zs, FrameCtl ctl)
+__device__ __forceinline__ void frames_g_impl(ZMQG_FRAMES_PARAMS)
 {
-    static_assert(G == 1 || G == 2 || G == 4, "lanes per frame");
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lanes per frame");
     const bool lb = DEC && rp.lb_flag != nullptr;
     unsigned long long clk0 = 0, rclk0 = 0;
     if (rp.clk) {
@@ -597,9 +609,9 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0; // the next call's list (the previous body has finished with it)
-    const uint32_t gl = wg * kFramesBS + threadIdx.x;
+    const uint32_t gl = (wg - ctl.split_wg) * kFramesBS + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t i = gl / G, q = gl % G;
+    const uint32_t i = ctl.split_n + gl / G, q = gl % G;
     const uint32_t gbase = lane - q; // the group's lane 0
     const bool valid = i < n;
     const uint32_t ii = valid ? i : n - 1;
@@ -1032,6 +1044,12 @@ __global__ __launch_bounds__(kFramesBS) void k_frames(
     }
 }
 
+template <bool DEC, int G, class BigOp>
+__global__ __launch_bounds__(kFramesBS) void k_frames(ZMQG_FRAMES_PARAMS)
+{
+    frames_g_impl<DEC, G, BigOp>(ZMQG_FRAMES_ARGS);
+}
+
 // Prefetch of words 1..16 of window w of a stream read in order (word 0 is
 // the previous window's word 16): dd[k] = the aligned word at A4 + 64w +
 // 4(k+1) (kept apart from word 0 so that they are an even register tuple),
@@ -1167,14 +1185,11 @@ template <bool DEC, class BigOp>
 #else
 #define ZMQG_SEQ_ATTR
 #endif
-__global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
-    uint32_t n, const uint32_t *__restrict__ sid, const uint64_t *__restrict__ nonce, const uint8_t *__restrict__ flags,
-    const uint64_t *__restrict__ in_off, const uint32_t *__restrict__ len, const uint8_t *__restrict__ in,
-    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, const DevSession *__restrict__ sessions,
-    uint32_t max_sessions, uint32_t max_stream, uint8_t *__restrict__ flags_out, int32_t *__restrict__ status_out,
-    ReplayOut rp, BigOp big, ZState *__restrict__ zs, FrameCtl ctl)
+__device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
 {
     const bool lb = DEC && rp.lb_flag != nullptr;
+    // frames this body covers: all, or (k_frames_split) the first split_n
+    const uint32_t nlim = ctl.split_wg ? ctl.split_n : n;
     SEQ_STAMP(0u);
     __shared__ unsigned long long sh_wmax[kFramesWaves];
     __shared__ CallState sh_cs;
@@ -1197,8 +1212,8 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
     uint32_t x0[16], d0 = 0; // window 0's stream words (decode: the wire; encode: payload bytes 0..), word 16
     auto fetch = [&](uint32_t wgv) {
         i = wgv * kFramesBS + threadIdx.x;
-        valid = i < n;
-        ii = valid ? i : n - 1;
+        valid = i < nlim;
+        ii = valid ? i : nlim - 1;
         sid_ok = sid[ii] < max_sessions;
         s = sid_ok ? sid[ii] : 0u; // (a frame of an unknown session is not processed)
         const DevSession &ses = sessions[s];
@@ -1675,6 +1690,29 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(
             zero_bytes(dst, S - 33u);
         }
     }
+}
+
+template <bool DEC, class BigOp>
+__global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(ZMQG_FRAMES_PARAMS)
+{
+    frames_seq_impl<DEC, BigOp>(ZMQG_FRAMES_ARGS);
+}
+
+// Batches just above one wave per SIMD (slots < n <= 3 slots / 2): the
+// first split_n = slots frames one lane each (one wave on every SIMD), the
+// remainder GT lanes per frame, in the same launch.  A SIMD that also holds
+// a remainder wave then runs about ceil(17 / GT) windows more instead of a
+// whole second frame (k_frames_seq alone: +50 % at 70,000 x 1 KiB,
+// DESIGN.md section 3.1).  Workgroup order is frame order, so the
+// one-session replay look-back runs across the two bodies unchanged; the
+// host launches this only when the grid is co-resident (no tickets).
+template <bool DEC, int GT, class BigOp>
+__global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_split(ZMQG_FRAMES_PARAMS)
+{
+    if (blockIdx.x < ctl.split_wg)
+        frames_seq_impl<DEC, BigOp>(ZMQG_FRAMES_ARGS);
+    else
+        frames_g_impl<DEC, GT, BigOp>(ZMQG_FRAMES_ARGS);
 }
 
 } // namespace zmqg

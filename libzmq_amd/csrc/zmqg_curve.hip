@@ -228,7 +228,8 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
-    int frames_cap[5] = {0, 0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4, seq, lds
+    int frames_cap[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4,
+                                                  // seq, lds, split 2, 4, 8
     int force_g = -1;                 // ZMQG_FRAMES_G: frame-kernel variant override (experiments)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
@@ -2116,19 +2117,46 @@ struct ProfSpan {
 // choice is about spreading the keystream work evenly over the SIMDs:
 //   n <  slots/2      G = 4 lanes per frame (k_frames)
 //   n <  2 slots/3    G = 2
-//   n <= 3 slots/2    k_frames_seq (0), one lane per frame
+//   n <= slots        k_frames_seq (0), one lane per frame
+//   n <= 3 slots/2    k_frames_split (16 + GT): the first `slots` frames one
+//                     lane each, the remainder GT lanes each in the same
+//                     launch, GT the largest of 8, 4, 2 that keeps the
+//                     remainder within one wave per SIMD
 //   beyond            k_frames_lds (8), LDS-staged coalesced traffic
 // The thresholds are the measured crossovers of the 1 KiB sweep in
 // DESIGN.md section 3 (32,768 ... 131,072 frames, every variant forced).
-// ZMQG_FRAMES_G (0, 1, 2, 4, 8) forces one of these variants whatever the
-// batch size, so the parity tests cover every variant the rule can pick.
+// ZMQG_FRAMES_G (0, 1, 2, 4, 8, 18, 20, 24) forces one of these variants
+// whatever the batch size (a split needs more than `slots` frames: below,
+// k_frames_seq runs), so the parity tests cover every variant the rule can
+// pick.
+static uint64_t device_slots(const zmqg_ctx *ctx)
+{
+    return 256ull * (uint64_t) (ctx->cus > 0 ? ctx->cus : 256);
+}
+
+static int split_variant(const zmqg_ctx *ctx, uint32_t n)
+{
+    const uint64_t slots = device_slots(ctx), r = n - slots;
+    return r * 8 <= slots ? 24 : r * 4 <= slots ? 20 : 18;
+}
+
 int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 {
+    const uint64_t slots = device_slots(ctx);
     if (ctx->force_g >= 0)
-        return ctx->force_g;
-    const uint64_t slots = 256ull * (uint64_t) (ctx->cus > 0 ? ctx->cus : 256);
+        return ctx->force_g >= 16 && n <= slots ? 0 : ctx->force_g;
     const uint64_t n2 = 2ull * n, n3 = 3ull * n;
-    return n2 < slots ? 4 : n3 < 2 * slots ? 2 : n2 <= 3 * slots ? 0 : 8;
+    return n2 < slots ? 4 : n3 < 2 * slots ? 2 : n <= slots ? 0 : n2 <= 3 * slots ? split_variant(ctx, n) : 8;
+}
+
+// The grid of a frame-kernel launch (workgroups of kFramesBS threads).
+static uint64_t frames_grid(const zmqg_ctx *ctx, int G, uint32_t n)
+{
+    if (G >= 16) {
+        const uint64_t sn = device_slots(ctx);
+        return sn / kFramesBS + ((n - sn) * (uint64_t) (G - 16) + kFramesBS - 1) / kFramesBS;
+    }
+    return ((uint64_t) n * (G == 1 || G == 2 || G == 4 ? G : 1) + kFramesBS - 1) / kFramesBS;
 }
 
 // Workgroups of the decode frame kernel the device holds at once (occupancy
@@ -2136,26 +2164,49 @@ int lanes_per_frame(const zmqg_ctx *ctx, uint32_t n)
 // MI355X_MICROARCH.md, Residency), cached per variant.
 int frames_capacity(zmqg_ctx *ctx, int G)
 {
-    int &c = ctx->frames_cap[G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0 : G == 2 ? 1 : 2];
+    int &c = ctx->frames_cap[G == 24 ? 7 : G == 20 ? 6 : G == 18 ? 5 : G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0
+                             : G == 2 ? 1 : 2];
     if (c == 0) {
         int nb = 0;
-        hipError_t e = G == 8   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_lds<true, DecodeHead>, kFramesBS, 0)
-                       : G == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
-                       : G == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
-                       : G == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, kFramesBS, 0)
-                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 4, DecodeHead>, kFramesBS, 0);
+        hipError_t e =
+            G == 24  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_split<true, 8, DecodeHead>, kFramesBS, 0)
+            : G == 20 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_split<true, 4, DecodeHead>, kFramesBS, 0)
+            : G == 18 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_split<true, 2, DecodeHead>, kFramesBS, 0)
+            : G == 8  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_lds<true, DecodeHead>, kFramesBS, 0)
+            : G == 0  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
+            : G == 1  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
+            : G == 2  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, kFramesBS, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 4, DecodeHead>, kFramesBS, 0);
         c = (e == hipSuccess && nb > 0) ? nb * ctx->cus : -1;
     }
     return c;
 }
 
 template <bool DEC, class BigOp>
-void launch_frames(int G, uint32_t n, hipStream_t st, const uint32_t *sid, const uint64_t *nonce,
+void launch_frames(const zmqg_ctx *ctx, int G, uint32_t n, hipStream_t st, const uint32_t *sid, const uint64_t *nonce,
                    const uint8_t *flags, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
                    const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
                    uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs, FrameCtl ctl)
 {
-    const dim3 grid((uint32_t) (((uint64_t) n * (G == 1 || G == 2 || G == 4 ? G : 1) + kFramesBS - 1) / kFramesBS));
+    const dim3 grid((uint32_t) frames_grid(ctx, G, n));
+    if (G >= 16) {
+        // (the split points: ctl carries them into both bodies)
+        const uint32_t sn = (uint32_t) device_slots(ctx);
+        ctl.split_wg = sn / kFramesBS;
+        ctl.split_n = sn;
+#define ZMQG_LAUNCH_SPLIT(GT)                                                                                        \
+    hipLaunchKernelGGL((k_frames_split<DEC, GT, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, \
+                       len, in, out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, \
+                       zs, ctl)
+        if (G == 24)
+            ZMQG_LAUNCH_SPLIT(8);
+        else if (G == 20)
+            ZMQG_LAUNCH_SPLIT(4);
+        else
+            ZMQG_LAUNCH_SPLIT(2);
+#undef ZMQG_LAUNCH_SPLIT
+        return;
+    }
     if (G == 8) {
         hipLaunchKernelGGL((k_frames_lds<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
                            out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
@@ -2328,7 +2379,7 @@ int zmqg_ctx_create(int device, uint32_t max_sessions, zmqg_ctx **ctx_out)
     ctx->h_downgrade.assign(max_sessions, 0);
     if (const char *fg = getenv("ZMQG_FRAMES_G")) {
         const int g = atoi(fg);
-        if (g == 0 || g == 1 || g == 2 || g == 4 || g == 8)
+        if (g == 0 || g == 1 || g == 2 || g == 4 || g == 8 || g == 18 || g == 20 || g == 24)
             ctx->force_g = g;
     }
     hipError_t e = hipSetDevice(device);
@@ -2722,7 +2773,7 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         }
     }
     ProfSpan main(ctx, ZMQG_PROF_ENCODE_MAIN, st);
-    launch_frames<false>(G, nn, st, sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
+    launch_frames<false>(ctx, G, nn, st, sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
                          ctx->max_sessions, nullptr, nullptr, ReplayOut{},
                          EncodeHead{sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
                                     ctx->max_sessions, R, ctl.nonce_ctr},
@@ -2788,7 +2839,7 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
         out = w.stage + ((uintptr_t) out_user & 15u);
     }
     const uint32_t nn = (uint32_t) n;
-    const int G = lanes_per_frame(ctx, nn);
+    int G = lanes_per_frame(ctx, nn);
     const bool multi = ctx->sort_bits > 0;
     FrameCtl ctl{};
     ctl.post = w.post;
@@ -2821,12 +2872,15 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
         // A grid that fits the device at once can use blockIdx as the
         // look-back order (every workgroup becomes resident eventually,
         // whatever the dispatch order); a larger one takes tickets.
-        const uint64_t grid = ((uint64_t) nn * (G == 1 || G == 2 || G == 4 ? G : 1) + kFramesBS - 1) / kFramesBS;
-        rp.ordered = grid <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
+        // (a split launch needs that order: its two bodies are told apart by
+        // blockIdx; without it the batch runs one lane per frame)
+        if (G >= 16 && frames_grid(ctx, G, nn) > (uint64_t) frames_capacity(ctx, G))
+            G = 0;
+        rp.ordered = frames_grid(ctx, G, nn) <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
     }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_DECODE_MAIN, st);
-    launch_frames<true>(G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out, ctx->sessions,
+    launch_frames<true>(ctx, G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out, ctx->sessions,
                         ctx->max_sessions, flags_out, status_out, rp,
                         DecodeHead{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R,
                                    zflags, (const unsigned long long *) zwalk, (unsigned long long *) zres},

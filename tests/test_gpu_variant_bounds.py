@@ -1,11 +1,15 @@
 """The frame-kernel variant rule (zmqg_curve.hip lanes_per_frame: slots =
 CUs x 256 one-wave-per-SIMD lanes; n < slots/2 -> 4 lanes per frame, < 2/3
-slots -> 2, <= 1.5 slots -> k_frames_seq, above -> k_frames_lds) at both
-sides of every boundary, on the library's own choice (no forcing): each
-batch's wire bit-exact against the oracle (src/curve_mechanism_base.cpp:
-111-205) with device-assigned nonces, and its decode (one session: the
-in-kernel look-back) equal to the oracle's sequential decode, a replay and a
-tampered frame included."""
+slots -> 2, <= slots -> k_frames_seq, <= 1.5 slots -> k_frames_split (the
+first `slots` frames one lane each, the remainder 8, 4 or 2 lanes each in the
+same launch), above -> k_frames_lds) at both sides of every boundary, on the
+library's own choice (no forcing): each batch's wire bit-exact against the
+oracle (src/curve_mechanism_base.cpp:111-205) with device-assigned nonces,
+and its decode (one session: the in-kernel look-back, across the split's two
+bodies) equal to the oracle's sequential decode, a replay and a tampered
+frame included.  The split sizes also run with frames of up to 4.5 KiB (the
+remainder lanes' Poly1305 combine over 8 / 4 / 2 lanes) and with 1 KiB
+frames at 70,000 (DESIGN.md section 3.1's sweep row)."""
 import numpy as np
 import pytest
 
@@ -17,18 +21,25 @@ pytestmark = pytest.mark.gpu
 def _bounds(cus):
     slots = 256 * cus
     b = [slots // 2 - 1, slots // 2, (2 * slots - 1) // 3, (2 * slots - 1) // 3 + 1, 3 * slots // 2,
-         3 * slots // 2 + 1]
+         3 * slots // 2 + 1,
+         # k_frames_seq | split, and the split's remainder widths 8 | 4 | 2
+         slots, slots + 1, slots + slots // 8, slots + slots // 8 + 1, slots + slots // 4, slots + slots // 4 + 1]
     return b
 
 
-@pytest.mark.parametrize("which", range(6))
-def test_variant_boundaries_bitexact(torch_cuda, C, which):
+SMALL = [0, 1, 31, 64, 95, 130]
+MIXED = [0, 1, 33, 100, 500, 1000, 1024, 2000, 3000, 4000, 4575, 4576]  # (4575 | 4576: the frame kernel | the body kernel)
+
+
+@pytest.mark.parametrize("which,sizes", [(k, SMALL) for k in range(12)] + [(k, MIXED) for k in (7, 8, 9, 10, 11, 4)]
+                         + [(70000, [1024])])
+def test_variant_boundaries_bitexact(torch_cuda, C, which, sizes):
     torch = torch_cuda
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    n = _bounds(cus)[which]
-    rng = np.random.default_rng(100 + which)
+    n = _bounds(cus)[which] if which < 100 else which
+    rng = np.random.default_rng(100 + which + len(sizes))
     key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
-    lens = rng.choice([0, 1, 31, 64, 95, 130], n).astype(np.uint32)
+    lens = rng.choice(sizes, n).astype(np.uint32)
     flags = rng.choice([0, 1, 2, 3], n).astype(np.uint8)
     in_off = np.zeros(n, np.uint64)
     in_off[1:] = np.cumsum(lens.astype(np.uint64))[:-1]

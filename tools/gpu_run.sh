@@ -21,6 +21,10 @@
 #   cfg4             config 4 as the bench runs it, each frame-kernel variant forced
 #   twowave          one-lane kernels at one and two waves per SIMD over 64 MiB
 #   engine           the host-adapter tests (batcher, engine hook with epoll)
+#   sweep            frame kernels just above one wave per SIMD: the library's
+#                    choice (k_frames_split) against k_frames_seq forced
+#   pmc4             config-4 PMC passes (instruction mix, wave-cycle shares,
+#                    TA/TD) of the frame kernels, encode against decode
 # Every GPU step runs under its own time limit and the script stops at the
 # first failure.
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -115,6 +119,32 @@ twowave)
 engine)
   timeout -k 10 600 $PYTEST tests/test_host_adapter.py tests/test_gpu_notify.py -m gpu > gpurun_out/pytest_engine.log 2>&1
   rc=$?; tail -3 gpurun_out/pytest_engine.log; [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_engine.log | head -60; exit 1; }
+  ;;
+sweep)
+  for r in 1 2; do
+    for n in 65536 65537 70000 73728 73729 81920 81921 98304; do
+      kb --iters 20 --msgs $n --size 1024 --tag split-$n || exit 1
+      ZMQG_FRAMES_G=0 kb --iters 20 --msgs $n --size 1024 --tag seq-$n || exit 1
+    done
+  done
+  ;;
+pmc4)
+  O=gpurun_out/pmc4
+  mkdir -p $O
+  timeout -k 10 60 rocprofv3 --list-avail > $O/counters.txt 2>&1 || true
+  p=0
+  for C in "SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM" \
+           "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES SQ_INSTS_SMEM" \
+           "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE GRBM_TA_BUSY" \
+           "TA_DATA_STALLED_BY_TC_CYCLES_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum" ; do
+    p=$((p + 1))
+    timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $PWD/$O/p$p -o pmc -- \
+        python tools/kbench.py --msgs 16777216 --size 256 --sessions 1024 --sid-mod --iters 2 > $O/p$p.log 2>&1
+    rc=$?
+    # (an unknown counter name fails the pass at once; a kill or a crash ends the call)
+    case $rc in 0) ;; 124|134|137|139) echo "pmc4 pass $p: rc $rc"; tail -5 $O/p$p.log; exit 1 ;;
+                *) echo "pmc4 pass $p failed (rc $rc)"; tail -3 $O/p$p.log ;; esac
+  done
   ;;
 *)
   echo "unknown mode $MODE"; exit 2

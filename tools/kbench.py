@@ -22,6 +22,8 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--sessions", type=int, default=1)
 ap.add_argument("--tag", default=os.environ.get("ZMQG_CURVE_LIB", "default"))
 ap.add_argument("--wire-align", type=int, default=1, help="wire frames at multiples of this many bytes")
+ap.add_argument("--sid-mod", action="store_true", help="frame i on session i mod sessions (bench config 4) "
+                "instead of contiguous blocks")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 n, P = a.msgs, a.size
@@ -33,7 +35,7 @@ for s in range(a.sessions):
     enc.session_set(s, bytes((s + j) % 256 for j in range(32)), C.CLIENT_PREFIX, C.SERVER_PREFIX)
     dec.session_set(s, bytes((s + j) % 256 for j in range(32)), C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
 t = lambda x, d: torch.from_numpy(np.ascontiguousarray(x).view(d)).to(dev)
-sid = t((np.arange(n) * a.sessions // n).astype(np.uint32), np.int32)
+sid = t(((np.arange(n) % a.sessions) if a.sid_mod else (np.arange(n) * a.sessions // n)).astype(np.uint32), np.int32)
 flags = torch.zeros(n, dtype=torch.uint8, device=dev)
 in_off = t(np.arange(n, dtype=np.uint64) * P, np.int64)
 lens = t(np.full(n, P, np.uint32), np.int32)
