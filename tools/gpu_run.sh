@@ -39,7 +39,7 @@ case $MODE in
 suite)
   timeout -k 10 1000 $PYTEST tests -m gpu > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -3
-  [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_gpu.log | head -80; exit 1; }
+  if [ $rc -ne 0 ]; then grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_gpu.log | head -80; exit 1; fi
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
   ;;
 bench)
@@ -117,8 +117,11 @@ twowave)
   done
   ;;
 engine)
-  timeout -k 10 600 $PYTEST tests/test_host_adapter.py tests/test_gpu_notify.py -m gpu > gpurun_out/pytest_engine.log 2>&1
-  rc=$?; tail -3 gpurun_out/pytest_engine.log; [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_engine.log | head -60; exit 1; }
+  timeout -k 10 600 $PYTEST -s tests/test_host_adapter.py tests/test_gpu_notify.py tests/test_libzmq_interop.py \
+      > gpurun_out/pytest_engine.log 2>&1
+  rc=$?; tail -3 gpurun_out/pytest_engine.log
+  if [ $rc -ne 0 ]; then grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_engine.log | head -60; exit 1; fi
+  grep -E "^OK 4800|'msgs_per_s'" gpurun_out/pytest_engine.log || true
   ;;
 sweep)
   for r in 1 2; do
