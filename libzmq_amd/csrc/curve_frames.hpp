@@ -38,7 +38,7 @@
 #pragma once
 
 #ifndef ZMQG_FRAMES_ABLATE
-#define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: k_frames: 1 no Poly1305, 2 no stores, 4 no input shift; k_frames_seq: 8 no stores, 16 no loads, 32 no Salsa20, 64 no Poly1305, 128 stores to 64-byte-aligned places (whole lines), 256 loads from 64-byte-aligned places
+#define ZMQG_FRAMES_ABLATE 0 // timing/counting experiments only: k_frames: 1 no Poly1305, 2 no stores, 4 no input shift; k_frames_seq: 8 no stores, 16 no loads, 32 no Salsa20, 64 no Poly1305, 128 stores to 64-byte-aligned places (whole lines), 256 loads from 64-byte-aligned places; k_frames_lds: 512 no partial edge granules, 1024 the encode head as two aligned dwordx4
 #endif
 
 
