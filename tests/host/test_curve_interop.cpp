@@ -26,6 +26,22 @@
 // and its MORE flag, and prints "OK <messages> <parts> <msgs/s> <MB/s>".
 // ZMTP heartbeats (ZMQ_HEARTBEAT_IVL) run on both sides, so PING/PONG
 // commands go through the codec too (src/zmtp_engine.cpp:463, 479).
+//
+//   interop pub <endpoint> <ack_endpoint> - <seed> <heartbeat_ivl_ms>
+//   interop sub <endpoint> <ack_endpoint> - <seed> <heartbeat_ivl_ms>
+//
+// PUB/SUB over CURVE: the SUB side's subscriptions travel as ZMTP 3.1
+// SUBSCRIBE / CANCEL commands through the MESSAGE codec (msg_t::subscribe /
+// cancel, src/curve_mechanism_base.cpp:118-164 on the encoding side, the
+// other side's decode and src/xpub.cpp applying them), so a layout either
+// codec got wrong shows up as a filter that does not match.  The PUB binds
+// (CURVE server) and publishes rounds of "alpha", "beta" and "gamma" messages
+// until told to stop; the SUB connects (CURVE client), subscribes to
+// "alpha" and "beta", cancels "beta" once both arrive, then subscribes to
+// "gamma": it checks every payload, that nothing outside its subscriptions
+// ever arrives, that "beta" stops after the cancel and "gamma" starts after
+// its subscription, then tells the PUB to stop (the acknowledgement
+// connection) and prints "OK <received> <alpha> <beta> <gamma>".
 #include <zmq.h>
 
 #include <errno.h>
@@ -34,6 +50,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <vector>
 
@@ -102,6 +119,149 @@ static void setup_heartbeats (void *s_, int ivl_)
     CHECK (zmq_setsockopt (s_, ZMQ_HEARTBEAT_TTL, &ttl, sizeof ttl) == 0);
 }
 
+//  payload of round r of a topic: the topic, ':', 8 bytes of r, 100 bytes
+static void pub_message (uint64_t seed_, const char *topic_, uint64_t r_, std::vector<uint8_t> &m_)
+{
+    const size_t tl = strlen (topic_);
+    m_.assign (topic_, topic_ + tl);
+    m_.push_back (':');
+    for (int b = 0; b < 8; ++b)
+        m_.push_back ((uint8_t) (r_ >> (8 * b)));
+    uint64_t s = seed_ * 0x100000001b3ull + r_ * 4 + (uint64_t) tl;
+    for (size_t k = 0; k < 100; k += 8) {
+        const uint64_t v = splitmix (s);
+        for (size_t b = 0; b < 8 && k + b < 100; ++b)
+            m_.push_back ((uint8_t) (v >> (8 * b)));
+    }
+}
+
+static void *curve_client (void *ctx_, int type_)
+{
+    void *s = zmq_socket (ctx_, type_);
+    CHECK (s);
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_SERVERKEY, server_public, 40) == 0);
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_PUBLICKEY, client_public, 40) == 0);
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_SECRETKEY, client_secret, 40) == 0);
+    return s;
+}
+
+static void *curve_server (void *ctx_, int type_)
+{
+    void *s = zmq_socket (ctx_, type_);
+    CHECK (s);
+    const int one = 1;
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_SERVER, &one, sizeof one) == 0);
+    CHECK (zmq_setsockopt (s, ZMQ_CURVE_SECRETKEY, server_secret, 40) == 0);
+    return s;
+}
+
+static const char *const topics[3] = {"alpha", "beta", "gamma"};
+
+static int run_pub (void *ctx_, const char *ep_, const char *ack_ep_, uint64_t seed_, int ivl_)
+{
+    void *p = curve_server (ctx_, ZMQ_PUB);
+    setup_heartbeats (p, ivl_);
+    CHECK (zmq_bind (p, ep_) == 0);
+    void *a = curve_server (ctx_, ZMQ_PULL);
+    CHECK (zmq_bind (a, ack_ep_) == 0);
+    printf ("READY\n");
+    fflush (stdout);
+    std::vector<uint8_t> m;
+    const double t0 = now_s ();
+    uint64_t r = 0;
+    for (;; ++r) {
+        for (int t = 0; t < 3; ++t) {
+            pub_message (seed_, topics[t], r, m);
+            CHECK (zmq_send (p, &m[0], m.size (), 0) == (int) m.size ());
+        }
+        char ack[8];
+        const int rc = zmq_recv (a, ack, sizeof ack, ZMQ_DONTWAIT);
+        if (rc == 4 && memcmp (ack, "STOP", 4) == 0)
+            break;
+        if (now_s () - t0 > 60) {
+            fprintf (stderr, "FAIL: no STOP within 60 s\n");
+            return 1;
+        }
+        usleep (50);
+    }
+    CHECK (zmq_close (a) == 0);
+    CHECK (zmq_close (p) == 0);
+    CHECK (zmq_ctx_term (ctx_) == 0);
+    printf ("PUBLISHED %llu rounds\n", (unsigned long long) r + 1);
+    return 0;
+}
+
+static int run_sub (void *ctx_, const char *ep_, const char *ack_ep_, uint64_t seed_, int ivl_)
+{
+    void *s = curve_client (ctx_, ZMQ_SUB);
+    const int rcvtimeo = 30000;
+    CHECK (zmq_setsockopt (s, ZMQ_RCVTIMEO, &rcvtimeo, sizeof rcvtimeo) == 0);
+    setup_heartbeats (s, ivl_);
+    CHECK (zmq_connect (s, ep_) == 0);
+    CHECK (zmq_setsockopt (s, ZMQ_SUBSCRIBE, "alpha", 5) == 0);
+    CHECK (zmq_setsockopt (s, ZMQ_SUBSCRIBE, "beta", 4) == 0);
+    //  phases: 0 alpha + beta subscribed; 1 beta cancelled, waiting for it to
+    //  stop; 2 gamma subscribed, waiting for it to start; 3 done
+    int phase = 0;
+    uint64_t got[3] = {0, 0, 0}, since_cancel = 0, last_beta = 0, received = 0;
+    std::vector<uint8_t> want;
+    char buf[256];
+    while (phase < 3) {
+        const int rc = zmq_recv (s, buf, sizeof buf, 0);
+        if (rc < 0) {
+            fprintf (stderr, "FAIL: receive in phase %d: %s\n", phase, zmq_strerror (zmq_errno ()));
+            return 1;
+        }
+        int t = -1;
+        for (int k = 0; k < 3; ++k)
+            if ((size_t) rc > strlen (topics[k]) && memcmp (buf, topics[k], strlen (topics[k])) == 0
+                && buf[strlen (topics[k])] == ':')
+                t = k;
+        if (t < 0 || (t == 2 && phase < 2)) {
+            fprintf (stderr, "FAIL: message outside the subscriptions in phase %d\n", phase);
+            return 1;
+        }
+        uint64_t r = 0;
+        memcpy (&r, buf + strlen (topics[t]) + 1, 8);
+        pub_message (seed_, topics[t], r, want);
+        if ((size_t) rc != want.size () || memcmp (buf, &want[0], rc) != 0) {
+            fprintf (stderr, "FAIL: payload of %s round %llu\n", topics[t], (unsigned long long) r);
+            return 1;
+        }
+        ++got[t];
+        ++received;
+        if (t == 1)
+            last_beta = received;
+        if (phase == 0 && got[0] && got[1]) {
+            CHECK (zmq_setsockopt (s, ZMQ_UNSUBSCRIBE, "beta", 4) == 0); //  a CANCEL command
+            phase = 1;
+            since_cancel = received;
+        } else if (phase == 1 && received - last_beta >= 500 && received - since_cancel >= 500) {
+            //  (beta published in the same rounds stopped coming: the cancel
+            //  has been applied by the PUB side)
+            CHECK (zmq_setsockopt (s, ZMQ_SUBSCRIBE, "gamma", 5) == 0);
+            phase = 2;
+        } else if (phase == 2 && t == 2) {
+            phase = 3;
+        }
+        if (phase >= 2 && t == 1) {
+            //  (every round publishes alpha and beta together: 500 alphas in
+            //  a row mean the PUB has stopped queueing beta for this peer)
+            fprintf (stderr, "FAIL: beta after its cancel had taken effect\n");
+            return 1;
+        }
+    }
+    void *a = curve_client (ctx_, ZMQ_PUSH);
+    CHECK (zmq_connect (a, ack_ep_) == 0);
+    CHECK (zmq_send (a, "STOP", 4, 0) == 4);
+    CHECK (zmq_close (a) == 0);
+    CHECK (zmq_close (s) == 0);
+    CHECK (zmq_ctx_term (ctx_) == 0);
+    printf ("OK %llu %llu %llu %llu\n", (unsigned long long) received, (unsigned long long) got[0],
+            (unsigned long long) got[1], (unsigned long long) got[2]);
+    return 0;
+}
+
 int main (int argc, char **argv)
 {
     if (argc != 7) {
@@ -119,6 +279,10 @@ int main (int argc, char **argv)
 
     void *ctx = zmq_ctx_new ();
     CHECK (ctx);
+    if (strcmp (argv[1], "pub") == 0)
+        return run_pub (ctx, endpoint, ack_endpoint, seed, ivl);
+    if (strcmp (argv[1], "sub") == 0)
+        return run_sub (ctx, endpoint, ack_endpoint, seed, ivl);
     std::vector<std::vector<uint8_t> > parts;
     if (pull) {
         //  perf/local_thr.cpp, as the CURVE server (tests/test_security_curve.cpp)

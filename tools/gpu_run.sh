@@ -149,6 +149,36 @@ pmc4)
                 *) echo "pmc4 pass $p failed (rc $rc)"; tail -3 $O/p$p.log ;; esac
   done
   ;;
+pmc4b)
+  # config 4: the store ablations' counters, and VALU per frame against the
+  # frame's window count (k_frames_lds forced) for the fixed per-frame part
+  O=gpurun_out/pmc4b
+  mkdir -p $O
+  C="SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVES"
+  for L in default abl512 abl1024 abl1536; do
+    LIB=""; [ $L != default ] && LIB=$PWD/tools/bin/$L/libzmqg_curve.so
+    ZMQG_CURVE_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $PWD/$O/$L -o pmc -- \
+        python tools/kbench.py --msgs 16777216 --size 256 --sessions 1024 --sid-mod --iters 2 > $O/$L.log 2>&1 \
+        || { echo "pmc4b $L failed"; tail -5 $O/$L.log; exit 1; }
+  done
+  for P in 128 192 256 384 512 768; do
+    ZMQG_FRAMES_G=8 timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $PWD/$O/sz$P -o pmc -- \
+        python tools/kbench.py --msgs 1048576 --size $P --sessions 1024 --sid-mod --iters 2 > $O/sz$P.log 2>&1 \
+        || { echo "pmc4b size $P failed"; tail -5 $O/sz$P.log; exit 1; }
+  done
+  ;;
+probe)
+  # the per-message floor: one launch per request (launch_floor) against a
+  # resident kernel polling a doorbell in host memory (resident_probe)
+  timeout -k 10 120 ./tools/bin/launch_floor || exit 1
+  timeout -k 10 60 ./tools/bin/resident_probe || exit 1
+  ;;
+interop)
+  timeout -k 10 600 $PYTEST -s tests/test_libzmq_interop.py > gpurun_out/pytest_interop.log 2>&1
+  rc=$?; tail -3 gpurun_out/pytest_interop.log
+  if [ $rc -ne 0 ]; then grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_interop.log | head -60; exit 1; fi
+  grep -E "'msgs_per_s'|'gamma'" gpurun_out/pytest_interop.log || true
+  ;;
 *)
   echo "unknown mode $MODE"; exit 2
   ;;
