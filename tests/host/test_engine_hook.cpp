@@ -63,9 +63,14 @@
 
 static const char client_prefix[] = "CurveZMQMESSAGEC";
 static const char server_prefix[] = "CurveZMQMESSAGES";
-static const int n_conn = 16;
-static const int n_msgs = 300;
-static const int bad_conn = 3, bad_msg = 50;
+static int n_conn = 16;
+static int n_msgs = 300;
+static int bad_conn = 3, bad_msg = 50;
+//  "bench <connections> <messages> <size>": the same engines and threads as a
+//  throughput run -- fixed-size plain messages, no tampering, the batcher's
+//  default slots -- printing "RATE ..." 
+static bool bench_mode = false;
+static size_t bench_size = 1024;
 static const int watchdog_s = 60;
 
 static uint64_t rng_state = 0x2545f4914f6cdd1dull;
@@ -371,8 +376,16 @@ static void close_in_flight (const zmqg::curve_batcher_t::config_t &cfg_)
 
 static std::atomic<int> threads_done (0);
 
-int main ()
+int main (int argc, char **argv)
 {
+    if (argc == 5 && strcmp (argv[1], "bench") == 0) {
+        bench_mode = true;
+        n_conn = atoi (argv[2]);
+        n_msgs = atoi (argv[3]);
+        bench_size = (size_t) atol (argv[4]);
+        bad_conn = bad_msg = -1;
+        CHECK (n_conn > 0 && n_msgs > 0);
+    }
     //  a hung exchange ends the process (the exit code names it)
     std::thread watchdog ([] {
         for (int i = 0; i < watchdog_s * 10; ++i) {
@@ -385,10 +398,12 @@ int main ()
     });
 
     zmqg::curve_batcher_t::config_t cfg;
-    cfg.slot_msgs = 64;
-    cfg.slot_bytes = 64 << 10;
-    cfg.slots = 3;
-    close_in_flight (cfg);
+    if (!bench_mode) {
+        cfg.slot_msgs = 64;
+        cfg.slot_bytes = 64 << 10;
+        cfg.slots = 3;
+        close_in_flight (cfg);
+    }
 
     io_thread_t ta (cfg), tb (cfg);
     static const size_t sizes[] = {0, 1, 31, 32, 33, 100, 255, 256, 1000, 4000, 5000, 20000};
@@ -422,10 +437,10 @@ int main ()
         s.expect = c == bad_conn ? (size_t) bad_msg : (size_t) n_msgs;
         for (int m = 0; m < n_msgs; ++m) {
             zmqg::msg_buf_t msg;
-            msg.bytes.resize (sizes[rnd () % (sizeof sizes / sizeof sizes[0])]);
+            msg.bytes.resize (bench_mode ? bench_size : sizes[rnd () % (sizeof sizes / sizeof sizes[0])]);
             for (size_t j = 0; j < msg.bytes.size (); ++j)
                 msg.bytes[j] = (uint8_t) rnd ();
-            msg.flags = flag_set[rnd () % (sizeof flag_set / sizeof flag_set[0])];
+            msg.flags = bench_mode ? 0 : flag_set[rnd () % (sizeof flag_set / sizeof flag_set[0])];
             k.session.push_back (msg);
         }
         ta.add_fd (k.fd, &k, EPOLLOUT);
@@ -490,6 +505,14 @@ int main ()
     delete ta.hook;
     delete tb.hook;
     CHECK (zmqg_ctx_destroy (ta.ctx) == 0 && zmqg_ctx_destroy (tb.ctx) == 0);
+    if (bench_mode) {
+        const double msgs = (double) n_conn * n_msgs;
+        printf ("RATE conns %d msgs %d size %zu ms %.1f msgs_per_s %.0f payload_MB_per_s %.1f waits %ld/%ld "
+                "hook_wakes %ld/%ld\n",
+                n_conn, n_msgs, bench_size, dt * 1e3, msgs / dt, msgs * bench_size / dt / 1e6, ta.waits, tb.waits,
+                ta.hook_wakes, tb.hook_wakes);
+        return 0;
+    }
     printf ("OK %d waits %ld/%ld hook_wakes %ld/%ld ms %.1f\n", n_conn * n_msgs, ta.waits, tb.waits,
             ta.hook_wakes, tb.hook_wakes, dt * 1e3);
     return 0;

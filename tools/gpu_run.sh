@@ -90,6 +90,7 @@ zmtp)
   done
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $PWD/gpurun_out/zprof -o run --output-format csv -- \
       python -u tools/zmtp_bench.py > gpurun_out/zprof.log 2>&1 || { tail -20 gpurun_out/zprof.log; exit 1; }
+  find gpurun_out/zprof -name "*kernel_trace.csv" -delete
   ;;
 msg)
   timeout -k 10 300 $PYTEST tests/test_gpu_msg.py tests/test_host_adapter.py -m gpu > gpurun_out/pytest_msg.log 2>&1 \
@@ -166,12 +167,22 @@ pmc4b)
         python tools/kbench.py --msgs 1048576 --size $P --sessions 1024 --sid-mod --iters 2 > $O/sz$P.log 2>&1 \
         || { echo "pmc4b size $P failed"; tail -5 $O/sz$P.log; exit 1; }
   done
+  # (only the counter summaries come back: gpurun_out is capped)
+  find $O -name "*kernel_trace.csv" -delete
+  find $O -name "*agent_info.csv" -delete
   ;;
 probe)
   # the per-message floor: one launch per request (launch_floor) against a
   # resident kernel polling a doorbell in host memory (resident_probe)
   timeout -k 10 120 ./tools/bin/launch_floor || exit 1
   timeout -k 10 60 ./tools/bin/resident_probe || exit 1
+  ;;
+hookbench)
+  # the batched adapter end to end: two epoll I/O threads, socketpairs,
+  # GPU encode on one side and decode on the other (tests/host/test_engine_hook.cpp bench)
+  for a in "16 20000 1024" "64 5000 1024" "256 1500 1024" "64 20000 256"; do
+    timeout -k 10 90 ./tools/bin/engine_hook_bench bench $a || exit 1
+  done
   ;;
 interop)
   timeout -k 10 600 $PYTEST -s tests/test_libzmq_interop.py > gpurun_out/pytest_interop.log 2>&1

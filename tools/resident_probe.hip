@@ -50,13 +50,23 @@ __global__ __launch_bounds__(64) void k_resident(Ctl *ctl, const uint32_t *req, 
             break;
         if (d != last) {
             last = d;
-            const uint32_t words = __hip_atomic_load(&ctl->bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) / 4u;
-            // the request's bytes over PCIe, the result back (one word per
-            // lane per round: the access shape of a message in host memory)
-            for (uint32_t k = lane; k < words; k += 64u) {
-                const uint32_t v = __hip_atomic_load(req + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(resp + k, v ^ d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            const uint32_t bytes = __hip_atomic_load(&ctl->bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the request's bytes over PCIe, the result back: 16 bytes per
+            // lane per round, every round's loads issued before any is used
+            // (coherent host memory is not cached by the GPU, so plain loads
+            // after the doorbell's acquire see the host's writes)
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            const u4 *rq = (const u4 *) req;
+            u4 *rs = (u4 *) resp;
+            u4 v[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (16u * (lane + 64u * j) < bytes)
+                    v[j] = rq[lane + 64u * j];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if (16u * (lane + 64u * j) < bytes)
+                    rs[lane + 64u * j] = v[j] ^ d;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             if (lane == 0)
                 __hip_atomic_store(&ctl->done, d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -88,7 +98,7 @@ int main()
     CK(hipGetLastError());
     uint32_t seq = 0;
     bool ok = true;
-    for (uint32_t bytes : {4u, 256u, 1024u, 4096u}) {
+    for (uint32_t bytes : {16u, 256u, 1024u, 4096u}) {
         std::vector<double> us;
         for (int r = 0; r < 2200; ++r) {
             ++seq;
@@ -110,7 +120,7 @@ int main()
             }
             if (r >= 200)
                 us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
-            for (uint32_t k = 0; k < bytes / 4; k += 97)
+            for (uint32_t k = 0; k < (bytes < 16 ? 4 : bytes / 4); k += 97)
                 if (resp[k] != (req[k] ^ seq)) {
                     fprintf(stderr, "request %u: word %u wrong\n", seq, k);
                     ok = false;
