@@ -253,50 +253,6 @@ int zmqg_decode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
                          const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
                          uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts, void *stream);
 
-/* A decode batch and an independent encode batch of two other ctxs, queued
- * on one stream: the results are those of zmqg_decode_batch_ex(dec) followed
- * by zmqg_encode_batch_ex(enc) on `stream` (which is what the call does when
- * the pair does not qualify for one launch).  The two batches must not share
- * any output region, and the encode must not write what the decode reads.
- * This is the I/O thread's steady state when it pipelines (the reference's
- * stream engine decodes what arrived and encodes what is queued to send,
- * src/stream_engine_base.cpp:281-291 in_event, :331-348 out_event): the decode of
- * batch k and the encode of batch k+1 share one launch, so the CUs that
- * finish their decode frames early start on the encode instead of waiting for
- * the slowest.  One launch when: dec->ctx != enc->ctx, both batches one lane
- * per frame (about 2/3 to 1 wave slots' frames: 43,691 ... 65,536 on
- * MI355X), both with opts->max_len within the frame kernel (decode <= 4608,
- * encode <= 4565), the decode's ctx one session and without
- * ZMQG_OPT_VERIFY_FIRST.  Profiling: each ctx's MAIN and CALL spans then time
- * the shared launch. */
-typedef struct zmqg_decode_args {
-    zmqg_ctx *ctx;
-    uint64_t n;
-    const uint32_t *sid;
-    const uint64_t *in_off;
-    const uint32_t *wire_len;
-    const uint8_t *in;
-    const uint64_t *out_off;
-    uint8_t *out;
-    uint8_t *flags_out;
-    int32_t *status_out;
-    const zmqg_batch_opts *opts;
-} zmqg_decode_args;
-typedef struct zmqg_encode_args {
-    zmqg_ctx *ctx;
-    uint64_t n;
-    const uint32_t *sid;
-    const uint64_t *nonce;
-    const uint8_t *flags;
-    const uint64_t *in_off;
-    const uint32_t *len;
-    const uint8_t *in;
-    const uint64_t *out_off;
-    uint8_t *out;
-    const zmqg_batch_opts *opts;
-} zmqg_encode_args;
-int zmqg_duplex_batch(const zmqg_decode_args *dec, const zmqg_encode_args *enc, void *stream);
-
 /* Header pass of a sharded decode: writes
  * session_max_out[s] (max_sessions entries, device-accessible) = the largest
  * header-valid nonce among the n wire frames of session s (0 where none).

@@ -357,23 +357,7 @@ struct FrameCtl {
     // on frames [0, split_n) (split_n = split_wg x kFramesBS), the rest run the
     // G-lanes-per-frame body on frames [split_n, n); 0 in every other launch
     uint32_t split_wg, split_n;
-    // k_frames_duplex: this batch's workgroups are [part_wg0, part_wg0 +
-    // part_wgn) of the launch (two batches share it); 0, 0: the whole grid
-    uint32_t part_wg0, part_wgn;
 };
-
-// A workgroup's index, and the grid's size, as its own batch sees them
-// (k_frames_duplex runs two batches in one launch, each on its own range of
-// workgroups; every other launch is one batch on the whole grid).
-__device__ __forceinline__ uint32_t part_block(const FrameCtl &ctl)
-{
-    return blockIdx.x - ctl.part_wg0;
-}
-
-__device__ __forceinline__ uint32_t part_grid(const FrameCtl &ctl)
-{
-    return ctl.part_wgn ? ctl.part_wgn : gridDim.x;
-}
 
 // msg_t flags a received ZMTP frame adds to its decoded message: the
 // decoder's MORE / COMMAND (src/v2_decoder.cpp:35-41) ORed into the
@@ -400,10 +384,10 @@ __device__ __forceinline__ uint32_t frame_zbits(const BigOp &big, uint32_t i)
 }
 
 template <bool DEC, class BigOp>
-__device__ __forceinline__ void frame_result_copy(const BigOp &big, const FrameCtl &ctl)
+__device__ __forceinline__ void frame_result_copy(const BigOp &big)
 {
     if constexpr (DEC) {
-        if (part_block(ctl) == 0 && threadIdx.x == 0 && big.res_src)
+        if (blockIdx.x == 0 && threadIdx.x == 0 && big.res_src)
             for (int k = 0; k < 4; ++k)
                 big.res_dst[k] = big.res_src[k];
     }
@@ -482,8 +466,8 @@ __device__ __forceinline__ void call_state_count(ZState *zs)
 template <bool DEC>
 __device__ __forceinline__ void call_state_end(ZState *zs, const FrameCtl &ctl, const CallState &c, uint32_t n)
 {
-    if (part_block(ctl) == 0 && threadIdx.x == 0) {
-        while (__hip_atomic_load(&zs->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < part_grid(ctl))
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        while (__hip_atomic_load(&zs->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x)
             __builtin_amdgcn_s_sleep(2);
         __hip_atomic_store(&zs->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&zs->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -620,10 +604,10 @@ __device__ __forceinline__ void frames_g_impl(ZMQG_FRAMES_PARAMS)
     const bool use_ticket = lb && !rp.ordered && !(rp.dbg & 2);
     const CallState cs = call_state_begin<DEC>(zs, ctl, use_ticket);
     const uint32_t epoch = cs.epoch;
-    const uint32_t wg = use_ticket ? cs.ticket : part_block(ctl);
+    const uint32_t wg = use_ticket ? cs.ticket : blockIdx.x;
     const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
-    if (part_block(ctl) == 0 && threadIdx.x == 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0; // the next call's list (the previous body has finished with it)
     const uint32_t gl = (wg - ctl.split_wg) * kFramesBS + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
@@ -999,9 +983,9 @@ __device__ __forceinline__ void frames_g_impl(ZMQG_FRAMES_PARAMS)
             // (a grid of at most kFramesBS workgroups looks back over every
             // aggregate in one round and needs no inclusive values: no
             // publish, and no drain of this wave's last stores for it)
-            if (part_grid(ctl) > kFramesBS)
+            if (gridDim.x > kFramesBS)
                 lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
-            if (wg + 1 == part_grid(ctl)) { // _cn_peer_nonce after the batch
+            if (wg + 1 == gridDim.x) { // _cn_peer_nonce after the batch
                 *rp.peer = inc > psn ? inc : psn;
                 if (rp.smax)
                     *rp.smax = inc;
@@ -1027,7 +1011,7 @@ __device__ __forceinline__ void frames_g_impl(ZMQG_FRAMES_PARAMS)
                __builtin_amdgcn_s_getreg((31 << 11) | 4); // XCC_ID : HW_ID
     }
     call_state_end<DEC>(zs, ctl, cs, n);
-    frame_result_copy<DEC>(big, ctl);
+    frame_result_copy<DEC>(big);
     if (!DEC && valid && q == 0 && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
     if (!valid || q != 0 || !small)
@@ -1277,18 +1261,18 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
         c0.nbase = DEC ? 0ull : nonce_base(ctl);
     }
     if (!use_ticket)
-        fetch(part_block(ctl));
+        fetch(blockIdx.x);
     if (threadIdx.x == 0)
         sh_cs = c0;
     __syncthreads();
     const CallState cs = sh_cs;
     const uint32_t epoch = cs.epoch;
-    const uint32_t wg = use_ticket ? cs.ticket : part_block(ctl);
+    const uint32_t wg = use_ticket ? cs.ticket : blockIdx.x;
     if (use_ticket)
         fetch(wg);
     const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
-    if (part_block(ctl) == 0 && threadIdx.x == 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
 
     if (!DEC) {
@@ -1649,9 +1633,9 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
             // (a grid of at most kFramesBS workgroups looks back over every
             // aggregate in one round and needs no inclusive values: no
             // publish, and no drain of this wave's last stores for it)
-            if (part_grid(ctl) > kFramesBS)
+            if (gridDim.x > kFramesBS)
                 lookback_publish(rp.lb_flag + wg, rp.lb_inc + wg, inc, epoch, 2);
-            if (wg + 1 == part_grid(ctl)) {
+            if (wg + 1 == gridDim.x) {
                 *rp.peer = inc > psn ? inc : psn;
                 if (rp.smax)
                     *rp.smax = inc;
@@ -1669,7 +1653,7 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
         big(i, list_ctr, nbase);
     }
     call_state_end<DEC>(zs, ctl, cs, n);
-    frame_result_copy<DEC>(big, ctl);
+    frame_result_copy<DEC>(big);
     SEQ_STAMP(61u);
     if (!DEC && valid && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
@@ -1729,51 +1713,6 @@ __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_split(ZMQG_F
         frames_seq_impl<DEC, BigOp>(ZMQG_FRAMES_ARGS);
     else
         frames_g_impl<DEC, GT, BigOp>(ZMQG_FRAMES_ARGS);
-}
-
-// One frame batch's kernel arguments, kept together (k_frames_duplex takes
-// two).
-template <class BigOp>
-struct FrameBatch {
-    uint32_t n;
-    const uint32_t *sid;
-    const uint64_t *nonce;
-    const uint8_t *flags;
-    const uint64_t *in_off;
-    const uint32_t *len;
-    const uint8_t *in;
-    const uint64_t *out_off;
-    uint8_t *out;
-    const DevSession *sessions;
-    uint32_t max_sessions, max_stream;
-    uint8_t *flags_out;
-    int32_t *status_out;
-    ReplayOut rp;
-    BigOp big;
-    ZState *zs;
-    FrameCtl ctl;
-};
-#define ZMQG_BATCH_ARGS(b)                                                                                  \
-    b.n, b.sid, b.nonce, b.flags, b.in_off, b.len, b.in, b.out_off, b.out, b.sessions, b.max_sessions,        \
-        b.max_stream, b.flags_out, b.status_out, b.rp, b.big, b.zs, b.ctl
-
-// A decode batch and an independent encode batch in one launch
-// (zmqg_duplex_batch): workgroups [0, d.ctl.part_wgn) decode, the rest encode,
-// both one lane per frame.  The host gives the launch enough dynamic LDS
-// that a CU holds one of its workgroups at a time, so the encode's
-// workgroups start on each CU as soon as that CU's decode workgroup is done
-// -- the CUs that finish the decode early take the encode's first
-// workgroups -- instead of every CU idling until the slowest finishes (the
-// drain between two launches).  The decode's workgroups come first in
-// dispatch order and there are at most one per CU, so they are co-resident
-// and its one-session look-back runs in blockIdx order.
-template <class BigD, class BigE>
-__global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_duplex(FrameBatch<BigD> d, FrameBatch<BigE> e)
-{
-    if (blockIdx.x < d.ctl.part_wgn)
-        frames_seq_impl<true, BigD>(ZMQG_BATCH_ARGS(d));
-    else
-        frames_seq_impl<false, BigE>(ZMQG_BATCH_ARGS(e));
 }
 
 } // namespace zmqg

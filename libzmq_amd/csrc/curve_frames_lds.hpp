@@ -529,7 +529,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         big(i, list_ctr, nbase);
     }
     call_state_end<DEC>(zs, ctl, cs, n);
-    frame_result_copy<DEC>(big, ctl);
+    frame_result_copy<DEC>(big);
     SEQ_STAMP(61u);
     if (!DEC && valid && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;

@@ -2093,7 +2093,7 @@ struct ProfSpan {
     hipEvent_t a = nullptr;
     ProfSpan(zmqg_ctx *c, int k, hipStream_t s) : ctx(c), kind(k), st(s)
     {
-        if (k >= 0 && ctx->profiling && (a = pool_event(ctx)))
+        if (ctx->profiling && (a = pool_event(ctx)))
             (void) hipEventRecord(a, st);
     }
     void end()
@@ -2182,33 +2182,12 @@ int frames_capacity(zmqg_ctx *ctx, int G)
     return c;
 }
 
-// zmqg_duplex_batch: the two batch calls fill these instead of launching
-// their frame kernels, and the duplex launch runs both.
-struct FramesDefer {
-    FrameBatch<DecodeHead> dec;
-    FrameBatch<EncodeHead> enc;
-    bool have_dec = false, have_enc = false;
-};
-
 template <bool DEC, class BigOp>
 void launch_frames(const zmqg_ctx *ctx, int G, uint32_t n, hipStream_t st, const uint32_t *sid, const uint64_t *nonce,
                    const uint8_t *flags, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
                    const uint64_t *out_off, uint8_t *out, const DevSession *sessions, uint32_t max_sessions,
-                   uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs, FrameCtl ctl,
-                   FramesDefer *defer = nullptr)
+                   uint8_t *flags_out, int32_t *status_out, ReplayOut rp, BigOp big, ZState *zs, FrameCtl ctl)
 {
-    if (defer) {
-        const FrameBatch<BigOp> b{n,         sid,        nonce,      flags, in_off, len, in, out_off, out, sessions,
-                                  max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs, ctl};
-        if constexpr (DEC) {
-            defer->dec = b;
-            defer->have_dec = true;
-        } else {
-            defer->enc = b;
-            defer->have_enc = true;
-        }
-        return;
-    }
     const dim3 grid((uint32_t) frames_grid(ctx, G, n));
     if (G >= 16) {
         // (the split points: ctl carries them into both bodies)
@@ -2753,13 +2732,9 @@ __global__ __launch_bounds__(256) void k_verify_copy(uint32_t n, const uint8_t *
     }
 }
 
-// zmqg_encode_batch_ex; defer (zmqg_duplex_batch): the frame kernel's
-// arguments go there instead of a launch (the caller has checked that the
-// batch needs no other kernel after it)
-static int encode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce,
-                             const uint8_t *flags, const uint64_t *in_off, const uint32_t *len, const uint8_t *in,
-                             const uint64_t *out_off, uint8_t *out, const zmqg_batch_opts *opts, void *stream,
-                             FramesDefer *defer)
+int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
+                         const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
+                         uint8_t *out, const zmqg_batch_opts *opts, void *stream)
 {
     if (!ctx || check_n(n) || check_opts(opts))
         return -EINVAL;
@@ -2787,7 +2762,7 @@ static int encode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
         ctl.no_body = opts->max_len && opts->max_len <= kMaxFrameStream - 43u; // (no wrap near UINT64_MAX)
     }
     const BigRecords R{w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.chunk_end, w.list_frame};
-    ProfSpan call(ctx, defer ? -1 : ZMQG_PROF_ENCODE_CALL, st);
+    ProfSpan call(ctx, ZMQG_PROF_ENCODE_CALL, st);
     if (auto_nonce) {
         if (ctx->max_sessions == 1) {
             ctl.nonce_ctr = ctx->send; // in the frame kernel
@@ -2797,16 +2772,12 @@ static int encode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
             nonce = w.nonce;
         }
     }
-    const EncodeHead head{sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions, ctx->max_sessions, R,
-                          ctl.nonce_ctr};
-    if (defer) {
-        launch_frames<false>(ctx, G, nn, st, sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
-                             ctx->max_sessions, nullptr, nullptr, ReplayOut{}, head, w.zs, ctl, defer);
-        return 0;
-    }
     ProfSpan main(ctx, ZMQG_PROF_ENCODE_MAIN, st);
     launch_frames<false>(ctx, G, nn, st, sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
-                         ctx->max_sessions, nullptr, nullptr, ReplayOut{}, head, w.zs, ctl);
+                         ctx->max_sessions, nullptr, nullptr, ReplayOut{},
+                         EncodeHead{sid, nonce, flags, in_off, len, in, out_off, out, ctx->sessions,
+                                    ctx->max_sessions, R, ctl.nonce_ctr},
+                         w.zs, ctl);
     ZCHECK(ctx, hipGetLastError());
     main.end();
     if (!ctl.no_body) {
@@ -2822,13 +2793,6 @@ static int encode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     return 0;
 }
 
-int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
-                         const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
-                         uint8_t *out, const zmqg_batch_opts *opts, void *stream)
-{
-    return encode_batch_impl(ctx, n, sid, nonce, flags, in_off, len, in, out_off, out, opts, stream, nullptr);
-}
-
 int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
                       const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,
                       uint8_t *out, void *stream)
@@ -2841,8 +2805,7 @@ int zmqg_encode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
 static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,
                              const uint32_t *wire_len, const uint8_t *in, const uint64_t *out_off, uint8_t *out,
                              uint8_t *flags_out, int32_t *status_out, const zmqg_batch_opts *opts,
-                             const uint8_t *zflags, const ZmtpWalk *zwalk, zmqg_zmtp_result *zres, void *stream,
-                             FramesDefer *defer = nullptr)
+                             const uint8_t *zflags, const ZmtpWalk *zwalk, zmqg_zmtp_result *zres, void *stream)
 {
     if (!ctx || check_n(n) || check_opts(opts))
         return -EINVAL;
@@ -2915,17 +2878,13 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
             G = 0;
         rp.ordered = frames_grid(ctx, G, nn) <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
     }
-    const DecodeHead head{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R,
-                          zflags, (const unsigned long long *) zwalk, (unsigned long long *) zres};
-    if (defer) {
-        launch_frames<true>(ctx, G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out,
-                            ctx->sessions, ctx->max_sessions, flags_out, status_out, rp, head, w.zs, ctl, defer);
-        return 0;
-    }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_DECODE_MAIN, st);
     launch_frames<true>(ctx, G, nn, st, sid, nullptr, nullptr, in_off, wire_len, in, out_off, out, ctx->sessions,
-                        ctx->max_sessions, flags_out, status_out, rp, head, w.zs, ctl);
+                        ctx->max_sessions, flags_out, status_out, rp,
+                        DecodeHead{sid, in_off, wire_len, in, out_off, out, ctx->sessions, ctx->max_sessions, R,
+                                   zflags, (const unsigned long long *) zwalk, (unsigned long long *) zres},
+                        w.zs, ctl);
     ZCHECK(ctx, hipGetLastError());
     main.end();
     if (multi && (rc = replay_multi(ctx, nn, sid, st, smax)))
@@ -2970,105 +2929,6 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
 {
     return zmqg_decode_batch_ex(ctx, n, sid, in_off, wire_len, in, out_off, out, flags_out, status_out, nullptr,
                                 stream);
-}
-
-// zmqg_duplex_batch's one-launch form: both batches one lane per frame
-// (k_frames_seq's range), neither needing a kernel after its frame kernel
-// (bounded frames; the decode one session, without VERIFY_FIRST), and the
-// decode at most one workgroup per CU.
-static bool duplex_eligible(const zmqg_decode_args *d, const zmqg_encode_args *e)
-{
-    zmqg_ctx *dc = d->ctx, *ec = e->ctx;
-    if (dc == ec || dc->device != ec->device || d->n == 0 || e->n == 0 || check_n(d->n) || check_n(e->n))
-        return false;
-    const zmqg_batch_opts *dop = d->opts, *eop = e->opts;
-    if (!dop || !eop || check_opts(dop) || check_opts(eop))
-        return false;
-    if (!dop->max_len || dop->max_len > kMaxFrameStream || (dop->flags & ZMQG_OPT_VERIFY_FIRST) || dc->sort_bits > 0)
-        return false;
-    if (!eop->max_len || eop->max_len > kMaxFrameStream - 43u)
-        return false;
-    const uint32_t dn = (uint32_t) d->n, en = (uint32_t) e->n;
-    return lanes_per_frame(dc, dn) == 0 && lanes_per_frame(ec, en) == 0 && frames_grid(dc, 0, dn) <= (uint64_t) dc->cus;
-}
-
-// Dynamic LDS of a duplex launch: enough that a CU holds one of its
-// workgroups at a time (half the CU's LDS, less the kernel's static LDS, plus
-// 1 KiB).  ZMQG_DUPLEX_LDS overrides it in bytes (0: co-resident workgroups).
-static int duplex_lds(zmqg_ctx *ctx, size_t *dyn)
-{
-    static std::mutex mu;
-    static long cached = -1;
-    std::lock_guard<std::mutex> g(mu);
-    if (cached < 0) {
-        const void *k = (const void *) k_frames_duplex<DecodeHead, EncodeHead>;
-        long want;
-        if (const char *v = getenv("ZMQG_DUPLEX_LDS")) {
-            want = strtol(v, nullptr, 0);
-        } else {
-            hipFuncAttributes fa{};
-            int lds = 0;
-            ZCHECK(ctx, hipFuncGetAttributes(&fa, k));
-            ZCHECK(ctx, hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, ctx->device));
-            const long half = lds / 2;
-            want = half > (long) fa.sharedSizeBytes ? ((half - (long) fa.sharedSizeBytes) & ~1023l) + 1024 : 0;
-        }
-        if (want < 0)
-            want = 0;
-        if (want > 0)
-            ZCHECK(ctx, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int) want));
-        cached = want;
-    }
-    *dyn = (size_t) cached;
-    return 0;
-}
-
-int zmqg_duplex_batch(const zmqg_decode_args *d, const zmqg_encode_args *e, void *stream)
-{
-    if (!d || !e || !d->ctx || !e->ctx)
-        return -EINVAL;
-    if (!duplex_eligible(d, e) || getenv("ZMQG_DUPLEX_OFF")) {
-        int rc = decode_batch_impl(d->ctx, d->n, d->sid, d->in_off, d->wire_len, d->in, d->out_off, d->out,
-                                   d->flags_out, d->status_out, d->opts, nullptr, nullptr, nullptr, stream);
-        if (rc)
-            return rc;
-        return encode_batch_impl(e->ctx, e->n, e->sid, e->nonce, e->flags, e->in_off, e->len, e->in, e->out_off,
-                                 e->out, e->opts, stream, nullptr);
-    }
-    zmqg_ctx *dc = d->ctx, *ec = e->ctx;
-    hipStream_t st = (hipStream_t) stream;
-    size_t dyn = 0;
-    int rc = duplex_lds(dc, &dyn);
-    if (rc)
-        return rc;
-    FramesDefer df;
-    if ((rc = decode_batch_impl(dc, d->n, d->sid, d->in_off, d->wire_len, d->in, d->out_off, d->out, d->flags_out,
-                                d->status_out, d->opts, nullptr, nullptr, nullptr, stream, &df)))
-        return rc;
-    if ((rc = encode_batch_impl(ec, e->n, e->sid, e->nonce, e->flags, e->in_off, e->len, e->in, e->out_off, e->out,
-                                e->opts, stream, &df)))
-        return rc;
-    if (!df.have_dec || !df.have_enc)
-    {
-        snprintf(dc->last_error, sizeof(dc->last_error), "zmqg_duplex_batch: a batch was not deferred");
-        return -EIO;
-    }
-    const uint32_t gd = (uint32_t) frames_grid(dc, 0, (uint32_t) d->n), ge = (uint32_t) frames_grid(ec, 0, (uint32_t) e->n);
-    df.dec.ctl.part_wg0 = 0;
-    df.dec.ctl.part_wgn = gd;
-    df.enc.ctl.part_wg0 = gd;
-    df.enc.ctl.part_wgn = ge;
-    // (each ctx's MAIN and CALL spans time the one launch both batches share)
-    ProfSpan dcall(dc, ZMQG_PROF_DECODE_CALL, st), dmain(dc, ZMQG_PROF_DECODE_MAIN, st);
-    ProfSpan ecall(ec, ZMQG_PROF_ENCODE_CALL, st), emain(ec, ZMQG_PROF_ENCODE_MAIN, st);
-    hipLaunchKernelGGL((k_frames_duplex<DecodeHead, EncodeHead>), dim3(gd + ge), dim3(kFramesBS), dyn, st, df.dec,
-                       df.enc);
-    ZCHECK(dc, hipGetLastError());
-    emain.end();
-    ecall.end();
-    dmain.end();
-    dcall.end();
-    return 0;
 }
 
 int zmqg_session_max_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *in_off,

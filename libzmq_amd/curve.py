@@ -74,19 +74,6 @@ class BatchOpts(ctypes.Structure):  # zmqg_batch_opts
 
 _lib.zmqg_encode_batch_ex.argtypes = [_P, _U64] + [_P] * 8 + [ctypes.POINTER(BatchOpts), _P]
 _lib.zmqg_decode_batch_ex.argtypes = [_P, _U64] + [_P] * 8 + [ctypes.POINTER(BatchOpts), _P]
-class DecodeArgs(ctypes.Structure):  # zmqg_decode_args
-    _fields_ = [("ctx", _P), ("n", _U64)] + [(f, _P) for f in ("sid", "in_off", "wire_len", "inp", "out_off", "out",
-                                                               "flags_out", "status_out")] + \
-               [("opts", ctypes.POINTER(BatchOpts))]
-
-
-class EncodeArgs(ctypes.Structure):  # zmqg_encode_args
-    _fields_ = [("ctx", _P), ("n", _U64)] + [(f, _P) for f in ("sid", "nonce", "flags", "in_off", "length", "inp",
-                                                               "out_off", "out")] + \
-               [("opts", ctypes.POINTER(BatchOpts))]
-
-
-_lib.zmqg_duplex_batch.argtypes = [ctypes.POINTER(DecodeArgs), ctypes.POINTER(EncodeArgs), _P]
 _lib.zmqg_session_max_batch.argtypes = [_P, _U64] + [_P] * 6
 _lib.zmqg_encode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _U64, _P, _P, _U64]
 _lib.zmqg_decode_host.argtypes = [_P, _U64, _P, _P, _P, _P, _U64, _P, _P, _U64, _P, _P]
@@ -283,25 +270,6 @@ class CurveContext:
         self._check(_lib.zmqg_decode_batch_ex(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
                                               _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_decode_batch")
-
-    def duplex_batch(self, dec, enc, stream=None):
-        """zmqg_duplex_batch: this ctx's decode batch and the encode batch of
-        another ctx queued together (one launch when the pair qualifies).
-        dec: dict of decode_batch's arguments (sid, in_off, wire_len, inp,
-        out_off, out, flags_out, status_out, max_len); enc: (ctx, dict of
-        encode_batch's: sid, nonce, flags, in_off, length, inp, out_off, out,
-        max_len, status_out, nonce_auto)."""
-        ectx, e = enc
-        od = self._opts(dec.get("max_len", 0), None, None)
-        oe = self._opts(e.get("max_len", 0), e.get("status_out"), None, e.get("nonce_auto", False))
-        da = DecodeArgs(self._ctx, int(dec["sid"].numel()), *[_ptr(dec[k]) for k in (
-            "sid", "in_off", "wire_len", "inp", "out_off", "out", "flags_out", "status_out")],
-            ctypes.pointer(od[1]) if od else None)
-        ea = EncodeArgs(ectx._ctx, int(e["sid"].numel()), *[_ptr(e.get(k)) for k in (
-            "sid", "nonce", "flags", "in_off", "length", "inp", "out_off", "out")],
-            ctypes.pointer(oe[1]) if oe else None)
-        self._check(_lib.zmqg_duplex_batch(ctypes.byref(da), ctypes.byref(ea), _stream_handle(stream)),
-                    "zmqg_duplex_batch")
 
     def session_max_batch(self, sid, in_off, wire_len, inp, session_max_out, stream=None):
         """Header pass: session_max_out (int64, max_sessions entries) = each

@@ -25,9 +25,8 @@
 #                    choice (k_frames_split) against k_frames_seq forced
 #   pmc4             config-4 PMC passes (instruction mix, wave-cycle shares,
 #                    TA/TD) of the frame kernels, encode against decode
-#   duplex           tests/test_gpu_duplex.py, then tools/duplex_ab.py (pipelined
-#                    duplex launch against sequential encode + decode) with the
-#                    default dynamic LDS, co-resident (0), and the pair as two calls
+#   settle           tools/replay_series.py: the timed replay's step time,
+#                    replay after replay (clock ramp), 20- and 100-step graphs
 # Every GPU step runs under its own time limit and the script stops at the
 # first failure.
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -193,15 +192,9 @@ interop)
   if [ $rc -ne 0 ]; then grep -B5 -A30 "FAILED\|Error" gpurun_out/pytest_interop.log | head -60; exit 1; fi
   grep -E "'msgs_per_s'|'gamma'" gpurun_out/pytest_interop.log || true
   ;;
-duplex)
-  timeout -k 10 600 $PYTEST tests/test_gpu_duplex.py > gpurun_out/duplex_tests.log 2>&1
-  rc=$?; grep -E "passed|failed|error" gpurun_out/duplex_tests.log | tail -3
-  if [ $rc -ne 0 ]; then grep -B5 -A30 "FAILED\|Error" gpurun_out/duplex_tests.log | head -80; exit 1; fi
-  for r in 1 2; do
-    timeout -k 10 180 python -u tools/duplex_ab.py "$@" || exit 1
-    ZMQG_DUPLEX_LDS=0 timeout -k 10 180 python -u tools/duplex_ab.py "$@" || exit 1
-    ZMQG_DUPLEX_OFF=1 timeout -k 10 180 python -u tools/duplex_ab.py "$@" || exit 1
-  done
+settle)
+  timeout -k 10 180 python -u tools/replay_series.py --reps 60 || exit 1
+  timeout -k 10 180 python -u tools/replay_series.py --reps 30 --steps 100 || exit 1
   ;;
 *)
   echo "unknown mode $MODE"; exit 2
