@@ -23,10 +23,9 @@ JSON line fields beyond the driver contract:
   roofline      dominant kernel (decode frame kernel) achieved algorithmic HBM-read
                 GB/s vs the 8 TB/s peak.  HIP events cannot time a kernel
                 inside a replayed graph, so the per-launch durations come
-                from HIP events on the launch stream around each frame kernel
-                in an eager pass of K more steps run right after the timed
-                replay (the same kernels and inputs; a later stretch of the
-                GPU's power curve, DESIGN.md section 4);
+                from replays of the timed graph and of a graph of its
+                encodes alone, alternating, just before the timed replay
+                (graph_shares: decode = the difference per step);
                 traffic = PMC-measured HBM bytes per launch from
                 profiles/ if a PMC summary for this workload was committed;
                 valu = the same kernel against the VALU issue peak (the bound
@@ -63,6 +62,8 @@ def parse():
     p.add_argument("--settle-ms", type=float, default=40.0,
                    help="untimed replays of the captured steps before the timed one, until this much GPU time "
                         "has passed (the clock ramp under sustained load; 0: none)")
+    p.add_argument("--cold-pass", action="store_true",
+                   help="also time each frame kernel on inputs from HBM (roofline.cold_launch_pass)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-staged", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of CPU baseline sampling")
@@ -165,8 +166,11 @@ def main():
     # reference's get_and_inc_nonce per message), then decode of that wire.
     # max_len = P: the batcher knows its frames' lengths, and a bound within the
     # frame kernel's range skips the large-frame launches (include/zmqg_curve.h).
-    def step(st):
+    def step_enc(st):
         enc.encode_batch(sid, None, flags, in_off, lens, payload, out_off, wire, st, max_len=P, nonce_auto=True)
+
+    def step(st):
+        step_enc(st)
         dec.decode_batch(sid, out_off, wlen, wire, in_off, back, fl_out, st_out, st, max_len=W)
 
     for _ in range(args.warmup):
@@ -182,10 +186,11 @@ def main():
     # state lives on the device, so replays are exact) and replayed as one
     # launch: the host's per-kernel launch cost stays out of the timed region.
     # HIP events cannot time kernels inside a graph, so the per-launch kernel
-    # durations (roofline) come from HIP events on the launch stream around
-    # each frame kernel in an eager pass of K more steps right after the timed
-    # replay; that pass's step time is reported as eager_ms_per_step.
-    # --eager times the eager steps (events on) instead.
+    # durations (roofline) come from graph replays just before the timed one
+    # (graph_shares).  An eager pass of K more steps after the timed replay,
+    # with the ctx profiling hooks on, gives eager_ms_per_step and the call
+    # spans (roofline.hooked_eager).  --eager times the eager steps (events
+    # on) instead.
     graph = None
     if not args.eager:
         try:
@@ -222,6 +227,12 @@ def main():
         ms = s0.elapsed_time(s1)
         settle_t += ms
         settle_us.append(round(1e3 * ms / args.steps, 1))
+    # The frame kernels' per-launch durations at the timed replay's clock:
+    # replays alternating with an encode-only graph, between the settling and
+    # the timed replay (the device ramps down within milliseconds of idling,
+    # so after the timed replay's checks they would measure another clock).
+    if graph is not None:
+        enc_avg_s, dec_avg_s, shares = graph_shares(torch, dev, stream, graph, step_enc, args.steps)
     if graph is None:
         enc.set_profiling(True)
         dec.set_profiling(True)
@@ -271,6 +282,21 @@ def main():
     dec.set_profiling(False)
     assert int((st_out != 0).sum()) == 0
     assert torch.equal(back, payload)
+    # per-launch durations of the two frame kernels for the roofline, as they
+    # run in the timed replay (graph_shares, measured just before it); without
+    # a graph, the hooks' event pairs around each eager launch
+    if graph is None:
+        enc_avg_s = enc_body_ms / max(enc_body_n, 1) / 1e3
+        dec_avg_s = dec_body_ms / max(dec_body_n, 1) / 1e3
+        shares = None
+    assert int((st_out != 0).sum()) == 0 and torch.equal(back, payload)
+    cold = None
+    if args.cold_pass:
+        ce, cd = launch_pass(torch, dev, stream, enc, dec, args.steps, n, W, P, sid, flags, in_off, lens, payload,
+                             out_off, wlen, back, fl_out)
+        cold = {"encode_us": ce * 1e6, "decode_us": cd * 1e6,
+                "note": f"{args.steps} encodes into {args.steps} wire buffers, then their {args.steps} decodes, each "
+                        "run back to back between one event pair: inputs from HBM, not the MALL (launch_pass)"}
 
     total_msgs = n * args.steps * world
     gib = total_msgs * P / 2**30
@@ -280,8 +306,6 @@ def main():
     # roofline of the dominant kernel: the decode frame kernel.  Algorithmic HBM-read
     # bytes of decode per frame: wire W + sid 4 + offset 8 +
     # length 4 = P + 49.
-    dec_avg_s = dec_body_ms / max(dec_body_n, 1) / 1e3
-    enc_avg_s = enc_body_ms / max(enc_body_n, 1) / 1e3
     dec_read = n * (P + 49)
     achieved = dec_read / dec_avg_s / 1e9 if dec_avg_s > 0 else None
     # traffic: HBM read bytes per launch of the same kernel from the committed
@@ -338,8 +362,15 @@ def main():
                 "traffic_write": traffic_write, "valu": valu, "pmc_files": pmc_notes,
                 "algorithmic_bytes_per_launch": dec_read, "avg_launch_us": dec_avg_s * 1e6,
                 "encode_main_avg_us": enc_avg_s * 1e6,
-                "encode_call_avg_us": enc_call_ms / max(enc_body_n, 1) * 1e3,
-                "decode_call_avg_us": dec_call_ms / max(dec_body_n, 1) * 1e3,
+                "duration_source": "graph replays: (K-step replay - K-encode replay) / K for decode, the K-encode "
+                                   "replay / K for encode, medians of 5 alternating replays each, between the "
+                                   "settling and the timed replay (graph_shares)" if shares
+                                   else "event pairs around each eager launch",
+                "graph_shares": shares, "cold_launch_pass": cold,
+                "hooked_eager": {"decode_main_us": dec_body_ms / max(dec_body_n, 1) * 1e3,
+                                 "encode_main_us": enc_body_ms / max(enc_body_n, 1) * 1e3,
+                                 "decode_call_us": dec_call_ms / max(dec_body_n, 1) * 1e3,
+                                 "encode_call_us": enc_call_ms / max(enc_body_n, 1) * 1e3},
                 "path_read_frac": (n * (2 * P + 74)) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS * world
                 if world == 1 else None}
 
@@ -385,6 +416,78 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def graph_shares(torch, dev, stream, graph, step_enc, K, reps=5):
+    """Per-launch durations of the encode and decode frame kernels as they
+    run in the timed replay.  HIP events cannot time a kernel inside a
+    replayed graph, and an event pair around each eager launch also spans
+    its dispatch (~5 us), so: a second graph of the K
+    steps' encodes alone is captured, and the timed graph and it are
+    replayed alternately `reps` times each, every replay between one event
+    pair; encode = median(encode-only replay) / K, decode = (median(full
+    replay) - median(encode-only replay)) / K -- each a kernel plus its
+    launch gap inside a graph, the same inputs and the same cache state as
+    the timed steps (the encode-only replays advance the encoder's nonces;
+    the decoder accepts the higher ones that follow).  Returns (encode s,
+    decode s, the replay times)."""
+    ge = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(dev)
+    cap.wait_stream(stream)
+    with torch.cuda.graph(ge, stream=cap):
+        cs = torch.cuda.current_stream(dev)
+        for _ in range(K):
+            step_enc(cs)
+    torch.cuda.synchronize(dev)
+    ge.replay()  # (untimed: first-replay costs)
+    torch.cuda.synchronize(dev)
+
+    def timed(g):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        g.replay()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        return a.elapsed_time(b) / 1e3
+
+    full, enc_only = [], []
+    for _ in range(reps):
+        full.append(timed(graph))
+        enc_only.append(timed(ge))
+    med = lambda v: sorted(v)[len(v) // 2]
+    e = med(enc_only) / K
+    d = med(full) / K - e
+    return e, d, {"full_replay_ms": [round(1e3 * x, 4) for x in full],
+                  "encode_only_replay_ms": [round(1e3 * x, 4) for x in enc_only]}
+
+
+def launch_pass(torch, dev, stream, enc, dec, K, n, W, P, sid, flags, in_off, lens, payload, out_off, wlen, back,
+                fl_out):
+    """Per-launch durations of the two frame kernels on inputs read from HBM
+    (--cold-pass): K encodes of the batch into K wire buffers (fresh device nonces each),
+    back to back on the launch stream between one HIP event pair, then the K
+    decodes of those buffers in order (each a valid batch of the session),
+    between another; each kernel's duration = its pair's span / K.  (An
+    event pair around every single launch -- the ctx profiling hooks of the
+    eager pass, `hooked_eager` -- also spans that launch's dispatch, ~5 us
+    here: DESIGN.md section 4.)  Every decode's statuses and payload are
+    checked.  Returns (encode s, decode s)."""
+    wires = [torch.empty(n * W, dtype=torch.uint8, device=dev) for _ in range(K)]
+    sts = [torch.full((n,), -1, dtype=torch.int32, device=dev) for _ in range(K)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    torch.cuda.synchronize(dev)
+    ev[0].record(stream)
+    for w in wires:
+        enc.encode_batch(sid, None, flags, in_off, lens, payload, out_off, w, stream, max_len=P, nonce_auto=True)
+    ev[1].record(stream)
+    ev[2].record(stream)
+    for w, st in zip(wires, sts):
+        dec.decode_batch(sid, out_off, wlen, w, in_off, back, fl_out, st, stream, max_len=W)
+    ev[3].record(stream)
+    torch.cuda.synchronize(dev)
+    assert all(int((st != 0).sum()) == 0 for st in sts), "launch pass: decode failures"
+    assert torch.equal(back, payload), "launch pass: round trip mismatch"
+    return ev[0].elapsed_time(ev[1]) / K / 1e3, ev[2].elapsed_time(ev[3]) / K / 1e3
 
 
 def device_census(torch, world, local):

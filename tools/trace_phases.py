@@ -3,9 +3,9 @@
 kernel trace of it (tools/gpu_run.sh prof writes one): the runs of 2K
 back-to-back frame launches (graph replays: gaps under 20 us) in order --
 the untimed instantiation and settling replays, then the timed replay --
-and the eager pass of K steps after them.  Shows whether the line's
-roofline.avg_launch_us (HIP events in the eager pass) matches the kernels
-of the timed replay.
+the eager pass of K steps after them, and bench.py's launch pass (K encodes,
+then K decodes, back to back).  Shows whether the line's
+roofline.avg_launch_us matches the kernels of the timed replay.
 
   trace_phases.py <trace dir> [K]"""
 import csv
