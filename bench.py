@@ -402,7 +402,8 @@ def main():
     }
 
     if not args.no_configs:
-        result["configs"] = other_configs(C, torch, dev, local, rank, world, args.configs.split(","))
+        result["configs"] = other_configs(C, torch, dev, local, rank, world, args.configs.split(","),
+                                          settle_ms=args.settle_ms)
 
     if rank == 0 and world == 1 and not args.no_host_staged:
         result["host_paths"] = host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_off, lens,
@@ -580,20 +581,28 @@ def config_step(b):
                           max_len=b["bound"] + 33 if b["bound"] else 0)
 
 
-def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1):
+def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1, settle_ms=40.0):
     """BASELINE configs 3, 4, 5: encode (device-assigned nonces) + decode round
     trips of device-resident batches, every result checked, timed like the
     main line (barrier + synchronize, max over ranks); payload GiB/s of the
-    whole job."""
+    whole job.  Untimed warmup steps: at least `warmup`, and more until
+    settle_ms of GPU time has passed since the last idle gap (the clock ramp,
+    DESIGN.md section 4; the inputs' preparation idles the device)."""
     import torch.distributed as dist
     from libzmq_amd import shard
     out = {}
     for w in which:
         b = config_inputs(C, torch, dev, local, rank, w, world)
         name, S, scaling, n, total = b["name"], b["S"], b["scaling"], b["n"], b["total"]
-        for _ in range(warmup):
+        wu, gpu_ms = 0, 0.0
+        while wu < warmup or (gpu_ms < settle_ms and wu < 200):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             config_step(b)
-        torch.cuda.synchronize(dev)
+            e1.record()
+            torch.cuda.synchronize(dev)
+            gpu_ms += e0.elapsed_time(e1)
+            wu += 1
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
@@ -608,7 +617,8 @@ def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1):
         job_frames = n * world if scaling == "weak" else sum_over_ranks(n)
         out["config" + w] = {"workload": name, "scaling": scaling, "value": job_bytes / 2**30 * steps / dt,
                              "unit": "GiB/s", "msgs_per_s": job_frames * steps / dt, "ms_per_step": 1e3 * dt / steps,
-                             "frames_per_gpu": n, "sessions_per_gpu": S, "steps": steps, "warmup": warmup,
+                             "frames_per_gpu": n, "sessions_per_gpu": S, "steps": steps, "warmup": wu,
+                             "warmup_gpu_ms": gpu_ms,
                              "checked": "every frame: status 0, decoded payload == input; the same batch is "
                                         "oracle-checked by tests/test_gpu_bench_batches.py"}
         del b
