@@ -11,7 +11,7 @@ mkdir -p $O
 for c in FETCH_SIZE WRITE_SIZE; do
   t=$(echo $c | tr A-Z a-z | cut -d_ -f1)
   timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $PWD/$O/$t -o pmc -- \
-      python bench.py --eager --steps 3 --warmup 1 --no-cpu-baseline --no-host-staged --no-configs > $O/$t.log 2>&1 || { echo "bench pass $c failed"; exit 1; }
+      python bench.py --eager --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-host-staged --no-configs > $O/$t.log 2>&1 || { echo "bench pass $c failed"; exit 1; }
   timeout -s KILL 60 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $PWD/$O/${t}_cal -o pmc -- \
       ./tools/bin/framecopy > $O/${t}_cal.log 2>&1 || { echo "calibration pass $c failed"; exit 1; }
 done
