@@ -74,8 +74,21 @@ for _ in range(a.reps):
     e1.record(s)
     torch.cuda.synchronize()
     us.append(e0.elapsed_time(e1) * 1e3 / a.steps)
+# the same K steps launched eagerly from the host, back to back, right after
+# the settled replays (events around the whole sequence), then one more replay
+eager = []
+for _ in range(3):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g.replay()
+    e0.record(s)
+    for _ in range(a.steps):
+        step(s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    eager.append(round(e0.elapsed_time(e1) * 1e3 / a.steps, 1))
 ok = bool((st == 0).all().item()) and bool(torch.equal(back, payload))
 tail = sorted(us[len(us) // 2:])
 print(json.dumps({"msgs": n, "size": P, "steps_per_replay": a.steps, "reps_us": [round(u, 1) for u in us],
                   "first_us": us[0], "settled_median_us": tail[len(tail) // 2],
-                  "settled_gib_s": n * P / 2**30 / (tail[len(tail) // 2] * 1e-6), "ok": ok}), flush=True)
+                  "settled_gib_s": n * P / 2**30 / (tail[len(tail) // 2] * 1e-6),
+                  "eager_after_replay_us": eager, "ok": ok}), flush=True)
