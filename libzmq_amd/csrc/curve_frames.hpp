@@ -1655,6 +1655,14 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     call_state_end<DEC>(zs, ctl, cs, n);
     frame_result_copy<DEC>(big);
     SEQ_STAMP(61u);
+#if ZMQG_SEQ_STAMPS
+    // (diagnostic: where the wave ran -- XCC_ID : HW_ID, whose CU, SH, SE and
+    // SIMD fields tell which waves shared a CU or a SIMD)
+    if (rp.clk && (threadIdx.x & 63u) == 0)
+        rp.clk[64ull * (blockIdx.x * kFramesWaves + (threadIdx.x >> 6)) + 62u] =
+            ((unsigned long long) __builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+            __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
     if (!DEC && valid && ctl.enc_status)
         ctl.enc_status[i] = !sid_ok ? ZMQG_ERR_SESSION : over ? ZMQG_ERR_BOUND : 0;
     if (!valid || !small)

@@ -18,6 +18,9 @@
 #ifndef STAMP_SHMEM_KB
 #define STAMP_SHMEM_KB 0 // dynamic LDS requested per workgroup (unused; 84: one workgroup per CU)
 #endif
+#ifndef STAMP_REPS
+#define STAMP_REPS 3 // launches per direction; the last two are stamped (plain, then rotated offsets; more: the clock settles first)
+#endif
 #ifndef STAMP_LDS
 #define STAMP_LDS 0 // 1: stamp k_frames_lds instead of k_frames_seq
 #endif
@@ -27,6 +30,14 @@
 #define KFR k_frames_seq
 #endif
 using namespace zmqg;
+// the frame kernels' BigOp without big frames (the library's NoBigFrames
+// predates the decode's ZMTP hooks, which the kernels now read)
+struct StampNoBig {
+    const uint8_t *zflags = nullptr;
+    const unsigned long long *res_src = nullptr;
+    unsigned long long *res_dst = nullptr;
+    __device__ void operator()(uint32_t, unsigned long long *, uint64_t) const {}
+};
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
@@ -52,6 +63,15 @@ int main()
     uint64_t *d_nonce = (uint64_t *) dev(nonce.data(), 8 * n), *d_ioff = (uint64_t *) dev(ioff.data(), 8 * n),
              *d_ooff = (uint64_t *) dev(ooff.data(), 8 * n);
     uint8_t *d_flags = (uint8_t *) dev(flags.data(), n);
+    // the same frames, each workgroup given the data of the workgroup half a
+    // grid away (frame i at frame (i + n/2) % n's offsets): a second stamped
+    // launch with these tells a slow CU from slow data
+    std::vector<uint64_t> ioff_r(n), ooff_r(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        ioff_r[i] = ioff[(i + n / 2) % n];
+        ooff_r[i] = ooff[(i + n / 2) % n];
+    }
+    uint64_t *d_ioff_r = (uint64_t *) dev(ioff_r.data(), 8 * n), *d_ooff_r = (uint64_t *) dev(ooff_r.data(), 8 * n);
     uint8_t *d_pay, *d_wire, *d_back, *d_fl;
     int32_t *d_st;
     CHECK(hipMalloc(&d_pay, (size_t) n * P + 256));
@@ -73,32 +93,107 @@ int main()
     CHECK(hipMemset(d_v, 0, 32ull * n + 64));
     const size_t nwaves = n / 64;
     CHECK(hipMalloc(&d_clk, 8 * 64 * nwaves));
+    unsigned long long *d_clk2;
+    CHECK(hipMalloc(&d_clk2, 8 * 64 * nwaves));
     ReplayOut rp{};
     rp.vout = d_v;
     rp.psnap = d_v + n;
     rp.peer = d_v + 3 * n;
     const dim3 grid(n / kFramesBS);
     for (int dec = 0; dec < 2; ++dec) {
-        for (int rep = 0; rep < 3; ++rep) {
-            CHECK(hipMemset(d_clk, 0, 8 * 64 * nwaves));
-            rp.clk = rep == 2 ? d_clk : nullptr;
+        CHECK(hipMemset(d_clk, 0, 8 * 64 * nwaves));
+        CHECK(hipMemset(d_clk2, 0, 8 * 64 * nwaves));
+        for (int rep = 0; rep < STAMP_REPS; ++rep) { // back to back, one synchronise after
+            // the last launch stamped with the rotated offsets, the one before with the plain ones
+            const bool rot = rep == STAMP_REPS - 1;
+            rp.clk = rep == STAMP_REPS - 2 ? d_clk : rot ? d_clk2 : nullptr;
+            const uint64_t *io = rot ? d_ioff_r : d_ioff, *oo = rot ? d_ooff_r : d_ooff;
             if (!dec)
-                hipLaunchKernelGGL((KFR<false, NoBigFrames>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid, d_nonce,
-                                   d_flags, d_ioff, d_len, d_pay, d_ooff, d_wire, d_ses, 1u, 0xffffffffu, nullptr,
-                                   nullptr, rp, NoBigFrames{}, d_zs, FrameCtl{});
+                hipLaunchKernelGGL((KFR<false, StampNoBig>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid, d_nonce,
+                                   d_flags, io, d_len, d_pay, oo, d_wire, d_ses, 1u, 0xffffffffu, nullptr,
+                                   nullptr, rp, StampNoBig{}, d_zs, FrameCtl{});
             else
-                hipLaunchKernelGGL((KFR<true, NoBigFrames>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid,
-                                   (const uint64_t *) nullptr, (const uint8_t *) nullptr, d_ooff, d_wl, d_wire, d_ioff,
-                                   d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, NoBigFrames{}, d_zs, FrameCtl{});
-            CHECK(hipDeviceSynchronize());
+                hipLaunchKernelGGL((KFR<true, StampNoBig>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid,
+                                   (const uint64_t *) nullptr, (const uint8_t *) nullptr, oo, d_wl, d_wire, io,
+                                   d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, StampNoBig{}, d_zs, FrameCtl{});
         }
-        std::vector<unsigned long long> c(64 * nwaves);
+        CHECK(hipDeviceSynchronize());
+        std::vector<unsigned long long> c(64 * nwaves), c2(64 * nwaves);
         CHECK(hipMemcpy(c.data(), d_clk, 8 * 64 * nwaves, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(c2.data(), d_clk2, 8 * 64 * nwaves, hipMemcpyDeviceToHost));
+        {
+            // per workgroup: its slowest wave, in the plain launch (A) and the rotated one (B)
+            const size_t nb = nwaves / kFramesWaves;
+            std::vector<double> A(nb), B(nb);
+            size_t same_cu = 0;
+            for (size_t b = 0; b < nb; ++b) {
+                double a = 0, bb = 0;
+                for (uint32_t k = 0; k < kFramesWaves; ++k) {
+                    const size_t w = b * kFramesWaves + k;
+                    a = std::max(a, (double) (c[64 * w + 61] - c[64 * w]));
+                    bb = std::max(bb, (double) (c2[64 * w + 61] - c2[64 * w]));
+                }
+                A[b] = a, B[b] = bb;
+                same_cu += (c[64 * b * kFramesWaves + 62] & 0xffffff00ull) == (c2[64 * b * kFramesWaves + 62] & 0xffffff00ull);
+            }
+            auto corr = [&](int shift) {
+                double ma = 0, mb = 0, sab = 0, saa = 0, sbb = 0;
+                for (size_t b = 0; b < nb; ++b)
+                    ma += A[(b + shift) % nb] / nb, mb += B[b] / nb;
+                for (size_t b = 0; b < nb; ++b) {
+                    const double x = A[(b + shift) % nb] - ma, y = B[b] - mb;
+                    sab += x * y, saa += x * x, sbb += y * y;
+                }
+                return sab / sqrt(saa * sbb);
+            };
+            printf("  workgroups on the same CU in both launches: %zu of %zu; correlation of workgroup times, "
+                   "same workgroup index (same CU) %.2f, same data %.2f\n", same_cu, nb, corr(0), corr((int) nb / 2));
+        }
+        // placement (slot 62: XCC_ID : HW_ID): workgroups per CU, waves per
+        // SIMD, and the workgroups' durations by how many shared their CU
+        {
+            std::vector<unsigned long long> key(nwaves);
+            for (size_t w = 0; w < nwaves; ++w) {
+                const unsigned long long h = c[64 * w + 62];
+                const unsigned hw = (unsigned) h, xcc = (unsigned) (h >> 32) & 0xfu;
+                key[w] = ((unsigned long long) xcc << 16) | (((hw >> 13) & 7u) << 8) | (((hw >> 12) & 1u) << 4) |
+                         ((hw >> 8) & 0xfu); // XCC, SE, SH, CU
+            }
+            std::vector<std::pair<unsigned long long, size_t>> cu;
+            for (size_t b = 0; b < nwaves / kFramesWaves; ++b)
+                cu.push_back({key[b * kFramesWaves], b});
+            std::sort(cu.begin(), cu.end());
+            std::vector<int> share(nwaves / kFramesWaves, 1);
+            size_t ncu = 0;
+            for (size_t j = 0; j < cu.size();) {
+                size_t k = j;
+                while (k < cu.size() && cu[k].first == cu[j].first)
+                    ++k;
+                for (size_t q = j; q < k; ++q)
+                    share[cu[q].second] = (int) (k - j);
+                ++ncu;
+                j = k;
+            }
+            double sum[4] = {0}, cnt[4] = {0}, mx[4] = {0};
+            for (size_t b = 0; b < nwaves / kFramesWaves; ++b) {
+                double d = 0;
+                for (uint32_t k = 0; k < kFramesWaves; ++k)
+                    d = std::max(d, (double) (c[64 * (b * kFramesWaves + k) + 61] - c[64 * (b * kFramesWaves + k)]));
+                const int s = std::min(share[b], 3);
+                sum[s] += d, cnt[s] += 1, mx[s] = std::max(mx[s], d);
+            }
+            printf("  distinct CUs %zu for %zu workgroups; slowest wave of a workgroup by workgroups on its CU:", ncu,
+                   nwaves / kFramesWaves);
+            for (int s = 1; s < 4; ++s)
+                if (cnt[s])
+                    printf(" [%d%s: %.0f wg, mean %.0f, max %.0f]", s, s == 3 ? "+" : "", cnt[s], sum[s] / cnt[s], mx[s]);
+            printf("\n");
+        }
         // per slot: median over waves of (stamp - entry stamp), and of step deltas
         printf("%s: median cycles since entry per phase (min/median/max over waves)\n", dec ? "decode" : "encode");
         // every stamped slot, in order of its median time
         std::vector<std::pair<long long, int>> order;
-        for (int sl = 1; sl < 64; ++sl) {
+        for (int sl = 1; sl < 62; ++sl) {
             std::vector<long long> v;
             for (size_t w = 0; w < nwaves; ++w)
                 if (c[64 * w + sl])
