@@ -45,6 +45,27 @@ namespace zmqg {
 #ifndef ZMQG_LDS_SECTOR
 #define ZMQG_LDS_SECTOR 16 // output runs are aligned to this many bytes (16 or 64)
 #endif
+// Issue priority by phase.  Two waves share each SIMD here (two workgroups
+// per CU) and the arbiter favours the older one, so a wave that reaches its
+// descriptor and key loads, a step's DMA and stores, or its epilogue while the
+// other is deep in a keystream waits behind that keystream to issue them, and
+// its memory latency starts late.  With s_setprio 3 over those stretches and
+// 0 over the keystream the memory work of either wave goes out at once and
+// the other's VALU stream fills the wait: config 4 (16 Mi x 256 B, 1,024
+// sessions) 9.87-9.89 ms per encode+decode against 11.12-11.18 for no
+// priorities on one box; 3/1 gave 9.91-10.26, 2/0 10.52-10.56
+// (DESIGN.md section 3.1).
+#ifndef ZMQG_LDS_PRIO
+#define ZMQG_LDS_PRIO 2 // priority while issuing memory work / during the keystream: 0 none, 1 3/1, 2 3/0, 3 2/0
+#endif
+#define LDS_PRIO_MEM (ZMQG_LDS_PRIO == 3 ? 2 : 3)
+#define LDS_PRIO_KS (ZMQG_LDS_PRIO == 1 ? 1 : 0)
+// (s_setprio takes an immediate)
+#define LDS_PRIO(lv)                                                                                   \
+    do {                                                                                               \
+        if (ZMQG_LDS_PRIO)                                                                             \
+            __builtin_amdgcn_s_setprio(lv);                                                            \
+    } while (0)
 #ifndef ZMQG_LDS_INBUF
 #define ZMQG_LDS_INBUF 2 // input buffers per wave (1: refilled right after it is read)
 #endif
@@ -128,6 +149,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     __shared__ __attribute__((aligned(16))) uint8_t st_lds[kFramesWaves * kStWave];
     const bool lb = DEC && rp.lb_flag != nullptr;
     SEQ_STAMP(0u);
+    LDS_PRIO(LDS_PRIO_MEM);
     __shared__ unsigned long long sh_wmax[kFramesWaves];
     const CallState cs = call_state_begin<DEC>(zs, ctl, lb && !rp.ordered);
     const uint32_t epoch = cs.epoch;
@@ -337,6 +359,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         dma(1u);
 
     SEQ_STAMP(1u);
+    LDS_PRIO(LDS_PRIO_KS);
     // ---- step 0: window 0 (Poly1305 key, first 32 ciphertext bytes, header)
     PolyKey32 pk;
     Poly32 h = {0, 0, 0, 0, 0};
@@ -404,6 +427,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         // stores go out before the keystream, so a whole window hides them
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        LDS_PRIO(LDS_PRIO_MEM);
         if (t < 8u)
             SEQ_STAMP(44u + t);
         const bool act = t < nw;
@@ -426,6 +450,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         if (t + 1u < steps)
             dma(t + 1u);
         ring_store(t - 1u, g);
+        LDS_PRIO(LDS_PRIO_KS);
         if (t < 8u)
             SEQ_STAMP(52u + t);
         uint32_t ks[16];
@@ -487,6 +512,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
             SEQ_STAMP(36u + t);
     }
     SEQ_STAMP(60u);
+    LDS_PRIO(LDS_PRIO_MEM);
     if (steps > 0) {
         // the last window's granules, and the granules its last ub bytes
         // spill into (odd window: bytes beyond ring byte 128, copied first)

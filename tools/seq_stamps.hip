@@ -18,6 +18,15 @@
 #ifndef STAMP_SHMEM_KB
 #define STAMP_SHMEM_KB 0 // dynamic LDS requested per workgroup (unused; 84: one workgroup per CU)
 #endif
+#ifndef STAMP_N
+#define STAMP_N 65536 // frames (config 4: -DSTAMP_N=16777216 -DSTAMP_P=256 -DSTAMP_S=1024 -DSTAMP_LDS=1)
+#endif
+#ifndef STAMP_P
+#define STAMP_P 1024 // payload bytes per frame
+#endif
+#ifndef STAMP_S
+#define STAMP_S 1 // sessions, frame i on session i mod STAMP_S
+#endif
 #ifndef STAMP_REPS
 #define STAMP_REPS 3 // launches per direction; the last two are stamped (plain, then rotated offsets; more: the clock settles first)
 #endif
@@ -43,8 +52,10 @@ struct StampNoBig {
 
 int main()
 {
-    const uint32_t n = 65536, P = 1024, W = P + 33;
+    const uint32_t n = STAMP_N, P = STAMP_P, W = P + 33, NS = STAMP_S;
     std::vector<uint32_t> sid(n, 0), len(n, P), wl(n, W);
+    for (uint32_t i = 0; i < n; ++i)
+        sid[i] = i % NS; // (config 4: frame i on session i mod 1,024)
     std::vector<uint64_t> nonce(n), ioff(n), ooff(n);
     std::vector<uint8_t> flags(n, 0);
     for (uint32_t i = 0; i < n; ++i) {
@@ -81,8 +92,8 @@ int main()
     CHECK(hipMalloc(&d_fl, n));
     CHECK(hipMalloc(&d_st, 4 * n));
     DevSession *d_ses;
-    CHECK(hipMalloc(&d_ses, sizeof(DevSession)));
-    CHECK(hipMemset(d_ses, 0x11, sizeof(DevSession)));
+    CHECK(hipMalloc(&d_ses, NS * sizeof(DevSession)));
+    CHECK(hipMemset(d_ses, 0x11, NS * sizeof(DevSession)));
     ZState *d_zs;
     CHECK(hipMalloc(&d_zs, sizeof(ZState)));
     ZState z0{};
@@ -110,12 +121,12 @@ int main()
             const uint64_t *io = rot ? d_ioff_r : d_ioff, *oo = rot ? d_ooff_r : d_ooff;
             if (!dec)
                 hipLaunchKernelGGL((KFR<false, StampNoBig>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid, d_nonce,
-                                   d_flags, io, d_len, d_pay, oo, d_wire, d_ses, 1u, 0xffffffffu, nullptr,
+                                   d_flags, io, d_len, d_pay, oo, d_wire, d_ses, NS, 0xffffffffu, nullptr,
                                    nullptr, rp, StampNoBig{}, d_zs, FrameCtl{});
             else
                 hipLaunchKernelGGL((KFR<true, StampNoBig>), grid, dim3(kFramesBS), STAMP_SHMEM_KB * 1024, 0, n, d_sid,
                                    (const uint64_t *) nullptr, (const uint8_t *) nullptr, oo, d_wl, d_wire, io,
-                                   d_back, d_ses, 1u, 0xffffffffu, d_fl, d_st, rp, StampNoBig{}, d_zs, FrameCtl{});
+                                   d_back, d_ses, NS, 0xffffffffu, d_fl, d_st, rp, StampNoBig{}, d_zs, FrameCtl{});
         }
         CHECK(hipDeviceSynchronize());
         std::vector<unsigned long long> c(64 * nwaves), c2(64 * nwaves);
