@@ -151,58 +151,96 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     SEQ_STAMP(0u);
     LDS_PRIO(LDS_PRIO_MEM);
     __shared__ unsigned long long sh_wmax[kFramesWaves];
-    const CallState cs = call_state_begin<DEC>(zs, ctl, lb && !rp.ordered);
+    __shared__ CallState sh_cs;
+    const bool use_ticket = lb && !rp.ordered; // (kernel-uniform)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+
+    // The frame's descriptors, session key and first window (as in
+    // k_frames_seq): without a look-back ticket to take, the workgroup's
+    // frames are known at entry, so these loads go out before the call
+    // state's round trip instead of after it.
+    uint32_t i = 0, ii = 0, s = 0, L_in = 0;
+    bool valid = false, sid_ok = false, over = false;
+    const uint8_t *src = nullptr;
+    uint8_t *dst = nullptr;
+    uint32_t key[8];
+    uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
+    uint64_t A = 0, B = 0, nc = 0;
+    unsigned long long psn = 0; // decode: the session's peer nonce before the batch
+    int32_t status = 0;
+    uint32_t hw[3] = {0, 0, 0};
+    uint32_t x0[16]; // window 0's stream words (decode: the wire; encode: payload bytes 0..31)
+    auto fetch = [&](uint32_t wgv) {
+        i = wgv * kFramesBS + threadIdx.x;
+        valid = i < n;
+        ii = valid ? i : n - 1;
+        sid_ok = sid[ii] < max_sessions;
+        s = sid_ok ? sid[ii] : 0u; // (a frame of an unknown session is not processed)
+        const DevSession &ses = sessions[s];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            key[t] = DEC ? ses.dec_key[t] : ses.enc_key[t];
+        src = in + in_off[ii];
+        dst = out + out_off[ii];
+        L_in = len[ii];
+        over = frame_over<DEC>(ctl, L_in, out_off[ii]); // the caller's bounds broken
+        if (!DEC) {
+            if (!ctl.nonce_ctr) // (device-assigned nonces need the call state's base)
+                nc = nonce[ii];
+            hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
+            S = sid_ok && !over ? 32u + hl + L_in : 0u;
+            A = (uint64_t) (uintptr_t) src - 32u - hl;
+            B = (uint64_t) (uintptr_t) dst;
+            if (L_in >= 32u) { // payload bytes 0..31: two dwordx4 (and a dword when unaligned)
+                load_bytes_c<32>(src, x0);
+#pragma unroll
+                for (int k = 8; k < 16; ++k)
+                    x0[k] = 0;
+            } else {
+                load_window(src, (int) L_in, x0);
+            }
+        } else {
+            // the wire frame's first window: header, nonce, tag, 32 ciphertext bytes
+            A = (uint64_t) (uintptr_t) src;
+            uint32_t d[17];
+            frame_load_raw(A, 0, L_in, d);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                x0[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], (uint32_t) A & 3u);
+            B = (uint64_t) (uintptr_t) dst - 33u;
+            psn = rp.peer[s];
+        }
+    };
+    // the call state (see call_state_begin): thread 0's reads go out first,
+    // the frame's loads behind them, and the reads are waited for (to publish
+    // them in LDS) only after both are in flight
+    CallState c0{};
+    if (threadIdx.x == 0) {
+        c0.epoch = __hip_atomic_load(&zs->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c0.ticket = use_ticket ? atomicAdd(&zs->ticket, 1u) : 0u;
+        c0.nbase = DEC ? 0ull : nonce_base(ctl);
+    }
+    if (!use_ticket)
+        fetch(blockIdx.x);
+    if (threadIdx.x == 0)
+        sh_cs = c0;
+    __syncthreads();
+    const CallState cs = sh_cs;
     const uint32_t epoch = cs.epoch;
-    const uint32_t wg = lb && !rp.ordered ? cs.ticket : blockIdx.x;
+    const uint32_t wg = use_ticket ? cs.ticket : blockIdx.x;
+    if (use_ticket)
+        fetch(wg);
     const uint64_t nbase = cs.nbase;
     unsigned long long *const list_ctr = zs->list_ctr + (epoch & 1u);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         zs->list_ctr[(epoch & 1u) ^ 1u] = 0;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t i = wg * kFramesBS + threadIdx.x;
-    const bool valid = i < n;
-    const uint32_t ii = valid ? i : n - 1;
-    const bool sid_ok = sid[ii] < max_sessions;
-    const uint32_t s = sid_ok ? sid[ii] : 0u; // (a frame of an unknown session is not processed)
-    const DevSession &ses = sessions[s];
-    uint32_t key[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-        key[t] = DEC ? ses.dec_key[t] : ses.enc_key[t];
-    const uint8_t *src = in + in_off[ii];
-    uint8_t *dst = out + out_off[ii];
-    const uint32_t L_in = len[ii];
-    const bool over = frame_over<DEC>(ctl, L_in, out_off[ii]); // the caller's bounds broken
 
-    uint32_t S = 0, n0 = 0, n1 = 0, hl = 1;
-    uint64_t A = 0, B = 0;
-    int32_t status = 0;
-    uint32_t hw[3] = {0, 0, 0};
-    uint32_t x0[16]; // window 0's stream words (decode: the wire; encode: payload bytes 0..31)
     if (!DEC) {
-        const uint64_t nc = frame_nonce(nonce, ctl, nbase, ii);
+        if (ctl.nonce_ctr)
+            nc = nbase + ii;
         n0 = bswap32((uint32_t) (nc >> 32));
         n1 = bswap32((uint32_t) nc);
-        hl = plaintext_header(flags[ii], ses.downgrade_sub, hw);
-        S = sid_ok && !over ? 32u + hl + L_in : 0u;
-        A = (uint64_t) (uintptr_t) src - 32u - hl;
-        B = (uint64_t) (uintptr_t) dst;
-        if (L_in >= 32u) { // payload bytes 0..31: two dwordx4 (and a dword when unaligned)
-            load_bytes_c<32>(src, x0);
-#pragma unroll
-            for (int k = 8; k < 16; ++k)
-                x0[k] = 0;
-        } else {
-            load_window(src, (int) L_in, x0);
-        }
     } else {
-        // the wire frame's first window: header, nonce, tag, 32 ciphertext bytes
-        A = (uint64_t) (uintptr_t) src;
-        uint32_t d[17];
-        frame_load_raw(A, 0, L_in, d);
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            x0[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], (uint32_t) A & 3u);
         if (L_in < 64u)
             mask_tail(x0, (int) L_in);
         // mechanism_base.cpp:14-25, curve_mechanism_base.cpp:80-97
@@ -223,10 +261,9 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         B = (uint64_t) (uintptr_t) dst - 33u;
     }
     const bool small = valid && S <= max_stream;
-    unsigned long long vn = 0, wexcl = 0, psn = 0, wagg = 0;
+    unsigned long long vn = 0, wexcl = 0, wagg = 0;
     if (DEC) {
         vn = valid && status == 0 ? (((unsigned long long) bswap32(n0) << 32) | bswap32(n1)) : 0ull;
-        psn = rp.peer[s];
         if (valid && !lb) { // (several sessions: the replay tables' input)
             rp.vout[i] = vn;
             rp.psnap[i] = psn;
