@@ -1641,6 +1641,19 @@ __global__ __launch_bounds__(256) void k_post(ZState *__restrict__ zs, const Pos
 // The big-frame list (positions 0 .. n-1, built by the frame kernel's head
 // calls) is read from the call state: n = entries, total = body chunks.
 template <bool DEC>
+// Issue priority by phase, as in k_frames_lds (curve_frames_lds.hpp): 3 while
+// a wave issues a tile's loads, DMA and stores, 0 over its keystream, MAC and
+// finish.  Configs 3 / 5 on one box, two alternating rounds: 538 / 534 and
+// 590.5 / 590.2 GiB/s against 527 / 528 and 586 / 588 without (the body
+// kernel already keeps the SIMDs' VALU ~98 % busy at config 5).
+#ifndef ZMQG_BODY_PRIO
+#define ZMQG_BODY_PRIO 1 // 0: no priorities
+#endif
+#define BODY_PRIO(lv)                                                                                  \
+    do {                                                                                               \
+        if (ZMQG_BODY_PRIO)                                                                            \
+            __builtin_amdgcn_s_setprio(lv);                                                            \
+    } while (0)
 __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_body(
     ZState *__restrict__ zs, const uint32_t *__restrict__ chunk_end,
     const FrameHot *__restrict__ hot, const FramePow *__restrict__ pw, const FrameFin *__restrict__ fin,
@@ -1701,6 +1714,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile t's DMA (and everything before it)
         wave_lds_fence();
         ZSTAMP(1);
+        BODY_PRIO(3);
         const bool has_next = t + 1 < te;
         // ---- issue: next tile's records, the chunk-end window after it
         const uint32_t gn = 64 * (t + 1) + lane;
@@ -1793,8 +1807,10 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
                     outw[16 * tw + 16] = __builtin_amdgcn_alignbyte(0u, w[15], 4 - so);
             }
         };
+        BODY_PRIO(0);
         if (nwin > 0)
             window(0);
+        BODY_PRIO(3);
         ZSTAMP(2);
         // ---- setup: next tile's params and its DMA; locate the tile after it
         // (on the wave's last tile this sets up an all-idle tile: no DMA)
@@ -1812,6 +1828,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
         }
         const FrameLook lk2 = window_find(ce2, lo2, n, 64 * (t + 2) + lane);
         ZSTAMP(3);
+        BODY_PRIO(0);
         if (nwin > 1)
             window(1);
         fe hf = poly32_to_fe(h);
@@ -1821,6 +1838,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
             v[q] = hf.l[q];
         wave_lds_fence();
         ZSTAMP(4);
+        BODY_PRIO(3);
         // ---- store: coalesced interior granules, then this lane's edges
         if (ZMQG_ABLATE != 5) // (timing experiments only)
         {
@@ -1859,6 +1877,7 @@ __global__ __launch_bounds__(kBodyThreads) __attribute__((amdgpu_waves_per_eu(2)
             }
         }
         ZSTAMP(5);
+        BODY_PRIO(0);
         // ---- finish: Poly1305 combine and tag / status
 #pragma unroll
         for (int q = 0; q < 4; ++q)
