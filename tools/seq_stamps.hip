@@ -204,7 +204,9 @@ int main()
         printf("%s: median cycles since entry per phase (min/median/max over waves)\n", dec ? "decode" : "encode");
         // every stamped slot, in order of its median time
         std::vector<std::pair<long long, int>> order;
-        for (int sl = 1; sl < 62; ++sl) {
+        for (int sl = 1; sl < 64; ++sl) {
+            if (sl == 62)
+                continue; // (the wave's placement, not a time)
             std::vector<long long> v;
             for (size_t w = 0; w < nwaves; ++w)
                 if (c[64 * w + sl])
