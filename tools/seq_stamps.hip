@@ -3,8 +3,14 @@
 // window 0 (1), after it (2), at the start of step t (3+t) and after the
 // wait for step t's input words (24+t), after the loop (60), at the end
 // (61); for steps 1..7 also after the input words are in (44+t), before the
-// stores (52+t) and after them (36+t).  Config-2 shape: 65,536 frames of 1 KiB, encode then decode.
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DZMQG_SEQ_STAMPS=1 -o tools/bin/seq_stamps tools/seq_stamps.hip
+// stores (52+t) and after them (36+t); slot 62 holds the wave's placement
+// (XCC_ID : HW_ID, k_frames_seq).  Default shape config 2 (65,536 frames of
+// 1 KiB, one session), encode then decode; STAMP_N / STAMP_P / STAMP_S set
+// another (config 4 below).  STAMP_REPS launches per direction back to back
+// (the clock settles), the last two stamped: the second with every
+// workgroup given the data of the one half a grid away, and the two
+// compared (slow CU or slow data).
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DZMQG_SEQ_STAMPS=1 -DSTAMP_REPS=400 -o tools/bin/seq_stamps tools/seq_stamps.hip
 // (add -DSTAMP_LDS=1 for k_frames_lds: slots 3+t step start, 44+t after the
 // wait, 52+t after the DMA and store issue, 24+t after keystream and MAC,
 // 36+t after the ring write)
