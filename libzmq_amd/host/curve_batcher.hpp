@@ -133,6 +133,8 @@ class curve_batcher_t
 
     size_t queued () const;    //  messages submitted and not yet launched
     size_t in_flight () const; //  messages launched and not yet delivered
+    //  slots launched and not yet delivered
+    size_t batches_in_flight () const { return _flight.size (); }
 
   private:
     enum kind_t

@@ -113,6 +113,9 @@ class curve_io_hook_t : private curve_sink_t
     //  launch and wait for everything queued (shutdown, tests)
     int drain ();
     size_t outstanding () const;
+    //  launched batches whose results have not been delivered yet (a poller
+    //  that holds new messages back while the device is busy uses it)
+    size_t batches_in_flight () const { return _batcher.batches_in_flight (); }
 
   private:
     friend class curve_engine_link_t;
@@ -163,6 +166,9 @@ class curve_engine_link_t
 
     size_t sends_in_flight () const { return _send_pending; }
     size_t receives_in_flight () const { return _recv_pending; }
+    //  results delivered and not yet taken by next_encoded / next_decoded
+    size_t encoded_queued () const { return _encoded.size (); }
+    size_t decoded_queued () const { return _decoded.size (); }
 
   private:
     friend class curve_io_hook_t;

@@ -123,6 +123,15 @@ class curve_encoding_t
         return _gpu.get_precom_buffer ();
     }
 
+    //  the connection's device session for the batched engine path
+    //  (zmq_curve_engine.hpp), NULL when it has no session slot.  Encodes and
+    //  decodes through it share this object's nonces and the device's peer
+    //  nonce, so the two paths can follow one another on a connection.
+    zmqg::curve_encoding_gpu_t *batched_codec ()
+    {
+        return _sid_errno ? NULL : &_gpu;
+    }
+
     typedef uint64_t nonce_t;
 
     nonce_t get_and_inc_nonce () { return _gpu.get_and_inc_nonce (); }

@@ -1,23 +1,32 @@
 #!/bin/sh
 # Builds the CURVE interop test of config 1 (BASELINE.json configs[0]: CURVE
-# PUSH/PULL over tcp://127.0.0.1, 1 KiB messages): two copies of the
+# PUSH/PULL over tcp://127.0.0.1, 1 KiB messages): three copies of the
 # reference libzmq and the test program tests/host/test_curve_interop.cpp
 # linked against each.
-#   stock  the reference's src/*.cpp compiled where they lie under
-#          /root/reference, CURVE over the image's libsodium 1.0.18
+#   stock  the reference's src/*.cpp, CURVE over the image's libsodium 1.0.18
 #          (/opt/conda), i.e. the reference's own codec;
 #   zmqg   the same sources with INTEGRATION.md section 2 applied
 #          (tests/host/libzmq_zmqg.patch, the ZMQ_USE_ZMQG_CURVE swap of
-#          curve_encoding_t) in a scratch copy outside the repository, plus
-#          libzmq_amd/host/curve_encoding_gpu.cpp, linked with
-#          libzmq_amd/libzmqg_curve.so: the MESSAGE codec on the GPU, the
-#          stream engine, I/O threads, handshake and sockets unchanged.
-# The reference's own build system is not run: g++ on its sources with the
-# test-only tests/host/ref_platform_full/platform.hpp in place of the
-# generated one; the optional transports (WS, TIPC, VMCI, VSOCK, NORM, PGM)
-# and GSSAPI are left out.  No reference source enters the repository;
-# output only into tests/host/_ref/libzmq/ (git-ignored, travels to the GPU
-# box, where /root/reference does not exist).  A no-op without the reference.
+#          curve_encoding_t) plus libzmq_amd/host/curve_encoding_gpu.cpp,
+#          linked with libzmq_amd/libzmqg_curve.so: the MESSAGE codec on the
+#          GPU, one device call per message, the stream engine, I/O threads,
+#          handshake and sockets unchanged;
+#   zmqgb  zmqg plus INTEGRATION.md section 3 (tests/host/libzmq_zmqg_batched.patch,
+#          ZMQ_USE_ZMQG_CURVE_BATCHED): the stream engine hands its messages
+#          to the I/O thread's batched codec (libzmq_amd/host/zmq_curve_engine.cpp,
+#          curve_engine_hook.cpp, curve_batcher.cpp), whose eventfd sits in the
+#          thread's poller.
+# Every copy also carries tests/host/libzmq_zmtp30_test.patch: a test-only
+# switch (ZMQG_TEST_ZMTP30 in the environment; unset, the library behaves as
+# the reference) that makes the side announce ZMTP 3.0, so its peer runs
+# handshake_v3_0 with downgrade_sub.
+# The reference's own build system is not run: g++ on its sources, in scratch
+# copies outside the repository, with the test-only
+# tests/host/ref_platform_full/platform.hpp in place of the generated one;
+# the optional transports (WS, TIPC, VMCI, VSOCK, NORM, PGM) and GSSAPI are
+# left out.  No reference source enters the repository; output only into
+# tests/host/_ref/libzmq/ (git-ignored, travels to the GPU box, where
+# /root/reference does not exist).  A no-op without the reference.
 set -e
 REF=${REF:-/root/reference}
 HERE=$(cd "$(dirname "$0")" && pwd)
@@ -25,9 +34,9 @@ ROOT=$(cd "$HERE/../.." && pwd)
 OUT="$HERE/_ref/libzmq"
 SODIUM=${SODIUM:-/opt/conda}
 JOBS=${MAX_JOBS:-8}
+HOST="$ROOT/libzmq_amd/host"
 [ -f "$REF/src/zmq.cpp" ] || { echo "build_libzmq: no reference sources at $REF; skipped"; exit 0; }
 [ -f "$SODIUM/include/sodium.h" ] || { echo "build_libzmq: no libsodium at $SODIUM; skipped"; exit 0; }
-mkdir -p "$OUT/stock/obj" "$OUT/zmqg/obj"
 
 # the core library's sources (optional transports and GSSAPI left out)
 list_sources () {
@@ -42,43 +51,68 @@ list_sources () {
 CXXFLAGS="-O2 -std=c++11 -fPIC -D_REENTRANT -D_THREAD_SAFE"
 export CXXFLAGS
 
-# compile $2 (a source) into $1/obj with include flags $3
-compile_all () {
-  out=$1; src=$2; inc=$3
-  list_sources "$src" | xargs -P "$JOBS" -I{} sh -c \
-    'f={}; o='"$out"'/obj/$(basename $f .cpp).o; [ "$o" -nt "$f" ] || g++ $CXXFLAGS '"$inc"' -c "$f" -o "$o"'
-}
-
-# --- stock -----------------------------------------------------------------
-INC_STOCK="-I$HERE/ref_platform_full -I$REF/include -I$REF/src -I$SODIUM/include"
-compile_all "$OUT/stock" "$REF" "$INC_STOCK"
-g++ -shared -o "$OUT/stock/libzmq.so.5" -Wl,-soname,libzmq.so.5 "$OUT"/stock/obj/*.o \
-  "$SODIUM/lib/libsodium.so.23" -Wl,-rpath,"$SODIUM/lib" -lpthread
-
-# --- zmqg: the patched copy, outside the repository -------------------------
 SCRATCH=$(mktemp -d /tmp/zmqg_libzmq.XXXXXX)
 trap 'rm -rf "$SCRATCH"' EXIT
-cp -rp "$REF/src" "$REF/include" "$SCRATCH/"   # (times kept: up-to-date objects are reused)
-patch -s -d "$SCRATCH" -p1 < "$HERE/libzmq_zmqg.patch"
-# a changed source must rebuild (the patch touches two files; the class
-# layout change reaches every file that includes them, so all are rebuilt
-# when the patch or the adapter header is newer than the library)
-if [ ! -f "$OUT/zmqg/libzmq.so.5" ] || [ "$HERE/libzmq_zmqg.patch" -nt "$OUT/zmqg/libzmq.so.5" ] \
-   || [ "$ROOT/libzmq_amd/host/zmq_curve_encoding.hpp" -nt "$OUT/zmqg/libzmq.so.5" ] \
-   || [ "$ROOT/libzmq_amd/host/curve_encoding_gpu.hpp" -nt "$OUT/zmqg/libzmq.so.5" ] \
-   || [ "$ROOT/include/zmqg_curve.h" -nt "$OUT/zmqg/libzmq.so.5" ]; then
-  rm -f "$OUT"/zmqg/obj/*.o
-fi
-INC_ZMQG="-DZMQ_USE_ZMQG_CURVE -I$HERE/ref_platform_full -I$SCRATCH/include -I$SCRATCH/src -I$SODIUM/include -I$ROOT/libzmq_amd/host"
-compile_all "$OUT/zmqg" "$SCRATCH" "$INC_ZMQG"
-g++ $CXXFLAGS -I"$ROOT/libzmq_amd/host" -c "$ROOT/libzmq_amd/host/curve_encoding_gpu.cpp" -o "$OUT/zmqg/obj/zmqg_curve_encoding_gpu.o"
-g++ -shared -o "$OUT/zmqg/libzmq.so.5" -Wl,-soname,libzmq.so.5 "$OUT"/zmqg/obj/*.o \
-  "$SODIUM/lib/libsodium.so.23" -Wl,-rpath,"$SODIUM/lib" \
-  -L"$ROOT/libzmq_amd" -lzmqg_curve -Wl,-rpath,/root/repo/libzmq_amd -L/opt/rocm/lib -Wl,-rpath-link,/opt/rocm/lib -lpthread
 
-# --- the test program, once per library (public zmq.h API only) -------------
-for v in stock zmqg; do
-  g++ -O2 -std=c++11 -Wall -Werror -I"$REF/include" -o "$OUT/interop_$v" "$HERE/test_curve_interop.cpp" \
-    "$OUT/$v/libzmq.so.5" -Wl,-rpath,/root/repo/tests/host/_ref/libzmq/$v -lpthread
-done
-echo "build_libzmq: $OUT/interop_stock $OUT/interop_zmqg"
+# variant <name> <defines> <patches...>: a scratch copy of the reference with
+# the patches applied, compiled into $OUT/<name>/libzmq.so.5.  All objects are
+# rebuilt when a patch or a header of ours is newer than the library (a class
+# layout change reaches every file that includes it); otherwise only sources
+# newer than their objects.
+variant () {
+  name=$1; defs=$2; shift 2
+  src="$SCRATCH/$name"
+  mkdir -p "$src" "$OUT/$name/obj"
+  cp -rp "$REF/src" "$REF/include" "$src/"   # (times kept: up-to-date objects are reused)
+  stale=0
+  [ -f "$OUT/$name/libzmq.so.5" ] || stale=1
+  for p in "$@"; do
+    patch -s -d "$src" -p1 < "$HERE/$p"
+    [ "$HERE/$p" -nt "$OUT/$name/libzmq.so.5" ] && stale=1
+  done
+  if [ -n "$defs" ]; then
+    for h in "$HOST"/*.hpp "$ROOT/include/zmqg_curve.h"; do
+      [ "$h" -nt "$OUT/$name/libzmq.so.5" ] && stale=1
+    done
+  fi
+  [ $stale = 1 ] && rm -f "$OUT/$name"/obj/*.o
+  inc="$defs -I$HERE/ref_platform_full -I$src/include -I$src/src -I$SODIUM/include -I$HOST"
+  list_sources "$src" | xargs -P "$JOBS" -I{} sh -c \
+    'f={}; o='"$OUT/$name"'/obj/$(basename $f .cpp).o; [ "$o" -nt "$f" ] || g++ $CXXFLAGS '"$inc"' -c "$f" -o "$o"'
+}
+
+# link <name> <extra sources of ours...>
+link () {
+  name=$1; shift
+  extra=""
+  for f in "$@"; do
+    o="$OUT/$name/obj/zmqg_$(basename "$f" .cpp).o"
+    g++ $CXXFLAGS $inc -c "$HOST/$f" -o "$o"
+    extra="$extra $o"
+  done
+  if [ -n "$extra" ]; then
+    # libzmqg_curve.so found from the library's own place in the tree
+    g++ -shared -o "$OUT/$name/libzmq.so.5" -Wl,-soname,libzmq.so.5 "$OUT/$name"/obj/*.o \
+      "$SODIUM/lib/libsodium.so.23" -Wl,-rpath,"$SODIUM/lib" \
+      -L"$ROOT/libzmq_amd" -lzmqg_curve -Wl,-rpath,'$ORIGIN/../../../../../libzmq_amd' \
+      -L/opt/rocm/lib -Wl,-rpath-link,/opt/rocm/lib -lpthread
+  else
+    g++ -shared -o "$OUT/$name/libzmq.so.5" -Wl,-soname,libzmq.so.5 "$OUT/$name"/obj/*.o \
+      "$SODIUM/lib/libsodium.so.23" -Wl,-rpath,"$SODIUM/lib" -lpthread
+  fi
+  # the test program (public zmq.h API only)
+  g++ -O2 -std=c++11 -Wall -Werror -I"$REF/include" -o "$OUT/interop_$name" "$HERE/test_curve_interop.cpp" \
+    "$OUT/$name/libzmq.so.5" -Wl,-rpath,'$ORIGIN/'"$name" -lpthread
+}
+
+variant stock "" libzmq_zmtp30_test.patch
+link stock
+
+variant zmqg "-DZMQ_USE_ZMQG_CURVE" libzmq_zmtp30_test.patch libzmq_zmqg.patch
+link zmqg curve_encoding_gpu.cpp
+
+variant zmqgb "-DZMQ_USE_ZMQG_CURVE -DZMQ_USE_ZMQG_CURVE_BATCHED" \
+  libzmq_zmtp30_test.patch libzmq_zmqg.patch libzmq_zmqg_batched.patch
+link zmqgb curve_encoding_gpu.cpp curve_batcher.cpp curve_engine_hook.cpp zmq_curve_engine.cpp
+
+echo "build_libzmq: $OUT/interop_stock $OUT/interop_zmqg $OUT/interop_zmqgb"

@@ -75,17 +75,31 @@ def run_pair(server_kind, client_kind, n=N, seed=11, heartbeat_ms=5):
             "msgs_per_s": float(f[3]), "MB_per_s": float(f[4])}
 
 
-def run_pubsub(pub_kind, sub_kind, seed=5, heartbeat_ms=5):
+def _env(**kv):
+    e = dict(os.environ)
+    e.update(kv)
+    return e
+
+
+def run_pubsub(pub_kind, sub_kind, seed=5, heartbeat_ms=5, pub_zmtp30=False):
     """PUB (CURVE server) as pub_kind, SUB (CURVE client) as sub_kind: the
     SUB's SUBSCRIBE / CANCEL commands cross the two codecs; returns the SUB's
-    counts (received, alpha, beta, gamma)."""
+    counts (received, alpha, beta, gamma).  pub_zmtp30: the PUB announces
+    ZMTP 3.0 (tests/host/libzmq_zmtp30_test.patch), so the SUB takes
+    handshake_v3_0 (src/zmtp_engine.cpp:383-393) and its CURVE mechanism
+    encodes subscriptions with downgrade_sub (src/curve_mechanism_base.cpp:
+    118-158); the SUB's stderr then carries the patch's trace line, which
+    the result reports as "downgraded"."""
     pub, sub = _exe(pub_kind), _exe(sub_kind)
     p, q = _ports()
     args = [f"tcp://127.0.0.1:{p}", f"tcp://127.0.0.1:{q}", "-", str(seed), str(heartbeat_ms)]
-    pp = subprocess.Popen([pub, "pub"] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    pub_env = _env(ZMQG_TEST_ZMTP30="1") if pub_zmtp30 else None
+    pp = subprocess.Popen([pub, "pub"] + args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                          env=pub_env)
     try:
         assert pp.stdout.readline().strip() == "READY"
-        s = subprocess.run([sub, "sub"] + args, capture_output=True, text=True, timeout=120)
+        s = subprocess.run([sub, "sub"] + args, capture_output=True, text=True, timeout=120,
+                           env=_env(ZMQG_TEST_ZMTP30_TRACE="1"))
         out, err = pp.communicate(timeout=60)
     finally:
         if pp.poll() is None:
@@ -96,11 +110,22 @@ def run_pubsub(pub_kind, sub_kind, seed=5, heartbeat_ms=5):
     f = s.stdout.strip().split()
     assert f[0] == "OK", s.stdout
     return {"pub": pub_kind, "sub": sub_kind, "received": int(f[1]), "alpha": int(f[2]), "beta": int(f[3]),
-            "gamma": int(f[4])}
+            "gamma": int(f[4]), "downgraded": "handshake_v3_0" in s.stderr}
 
 
 def test_stock_pubsub_subscribe_cancel():
-    print(run_pubsub("stock", "stock"))
+    r = run_pubsub("stock", "stock")
+    assert not r["downgraded"]
+    print(r)
+
+
+def test_stock_pubsub_downgraded_subscriptions():
+    """The harness for the ZMTP 3.0 cases on the CPU: a stock PUB announcing
+    3.0, a stock SUB that takes handshake_v3_0 and sends its subscriptions
+    downgraded -- the filter still applies exactly."""
+    r = run_pubsub("stock", "stock", pub_zmtp30=True)
+    assert r["downgraded"], r
+    print(r)
 
 
 def test_stock_pair_delivers_everything():
@@ -129,3 +154,47 @@ def test_gpu_codec_subscribe_cancel_interop(pub, sub):
     subscription.  Interop evidence for the command layouts the golden
     vectors restate (tests/golden/make_golden.py), not an oracle pin."""
     print(run_pubsub(pub, sub))
+
+
+# --- the batched codec inside the engine (INTEGRATION.md section 3) ---------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("server,client", [("zmqgb", "stock"), ("stock", "zmqgb"), ("zmqgb", "zmqgb"),
+                                           ("zmqgb", "zmqg")])
+def test_gpu_batched_codec_interoperates(server, client):
+    """The stream engine with the I/O thread's batched GPU codec
+    (tests/host/libzmq_zmqg_batched.patch): every message of config 1's
+    plan arrives byte-exact, MORE flags included, with heartbeats every 5 ms
+    (PING / PONG submitted in order with the messages), both CURVE roles,
+    against the stock codec and the per-message GPU codec."""
+    t0 = time.time()
+    r = run_pair(server, client)
+    r["wall_s"] = time.time() - t0
+    print(r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pub,sub", [("stock", "zmqgb"), ("zmqgb", "stock")])
+def test_gpu_batched_subscribe_cancel_interop(pub, sub):
+    """SUBSCRIBE / CANCEL through the batched codec in both directions: the
+    PUB applies exactly the SUB's subscriptions."""
+    r = run_pubsub(pub, sub)
+    assert not r["downgraded"]
+    print(r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pub,sub", [("stock", "zmqg"), ("zmqg", "stock"), ("stock", "zmqgb"),
+                                     ("zmqgb", "stock")])
+def test_gpu_downgraded_subscriptions_interop(pub, sub):
+    """A ZMTP 3.0 PUB (test switch): the SUB runs handshake_v3_0 and its
+    CURVE codec encodes SUBSCRIBE / CANCEL with downgrade_sub -- as a
+    message whose first byte is 1 / 0 (src/curve_mechanism_base.cpp:118-158)
+    -- which the PUB's codec decodes and src/xpub.cpp applies.  With the GPU
+    codec on the SUB side the device writes the downgraded layout and the
+    stock PUB's libsodium opens it; with the GPU codec on the PUB side it
+    opens the stock SUB's.  The filter applies exactly as in the 3.1 cases:
+    the downgrade_sub layout crosses the reference codec both ways."""
+    r = run_pubsub(pub, sub, pub_zmtp30=True)
+    assert r["downgraded"], r
+    print(r)
