@@ -234,10 +234,29 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  *                    would end past out_bytes fails with ZMQG_ERR_BOUND and
  *                    nothing of it is written; 0 is valid for a batch whose
  *                    frames carry no payload bytes).
- * A caller built against the struct without out_bytes passes the smaller
- * size and gets the old behaviour. */
+ *   flags            ZMQG_OPT_REPLAY_HOST (decode, with VERIFY_FIRST and
+ *                    verdict_in): the caller has already applied the header
+ *                    rules and the replay rule to the frames in batch order,
+ *                    as check_basic_command_structure and check_validity do
+ *                    (src/mechanism_base.cpp:14-25,
+ *                    src/curve_mechanism_base.cpp:80-106: the nonce must
+ *                    exceed the connection's peer nonce, which advances
+ *                    before the MAC), keeping the connections' peer nonces
+ *                    itself -- a host that sees every frame in order does
+ *                    this with one compare per frame.  The device then only
+ *                    authenticates and opens: it neither reads nor writes its
+ *                    sessions' peer nonces (zmqg_session_set_peer_nonce
+ *                    before a later call that does), and the call is two
+ *                    kernel launches instead of seven for several sessions.
+ *   verdict_in       with ZMQG_OPT_REPLAY_HOST: n entries (device-accessible),
+ *                    per frame 0 (open it) or the ZMQG_ERR_* code the host's
+ *                    rules gave it, which is then the frame's status (its
+ *                    payload region zero-filled, flags 0).
+ * A caller built against the struct without out_bytes (or verdict_in)
+ * passes the smaller size and gets the old behaviour. */
 #define ZMQG_OPT_NONCE_AUTO 1u
 #define ZMQG_OPT_VERIFY_FIRST 2u
+#define ZMQG_OPT_REPLAY_HOST 4u
 typedef struct zmqg_batch_opts {
     uint32_t size;
     uint32_t flags;
@@ -245,6 +264,7 @@ typedef struct zmqg_batch_opts {
     int32_t *status_out;
     uint64_t *session_max_out;
     uint64_t out_bytes;
+    const int32_t *verdict_in;
 } zmqg_batch_opts;
 int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint64_t *nonce, const uint8_t *flags,
                          const uint64_t *in_off, const uint32_t *len, const uint8_t *in, const uint64_t *out_off,

@@ -204,6 +204,7 @@ struct zmqg_ctx {
     DevSession *sessions = nullptr;
     unsigned long long *peer = nullptr; // [max_sessions]
     unsigned long long *send = nullptr; // [max_sessions] send nonces (_cn_nonce) for ZMQG_OPT_NONCE_AUTO
+    unsigned long long *zero_peer = nullptr; // [max_sessions] zeros: ZMQG_OPT_REPLAY_HOST's peer snapshot
     Workspace ws;
     ZmtpWs zw;
     // host staging for the *_host entry points
@@ -2086,6 +2087,16 @@ uint32_t body_grid(const zmqg_ctx *ctx)
     return kBodyWgPerCu * (ctx->cus > 0 ? (uint32_t) ctx->cus : 256u);
 }
 
+// ZMQG_OPT_REPLAY_HOST: a zeroed peer-nonce table for the frame kernels
+int ensure_zero_peer(zmqg_ctx *ctx, hipStream_t st)
+{
+    if (ctx->zero_peer)
+        return 0;
+    ZCHECK(ctx, hipMallocAsync((void **) &ctx->zero_peer, sizeof(unsigned long long) * ctx->max_sessions, st));
+    ZCHECK(ctx, hipMemsetAsync(ctx->zero_peer, 0, sizeof(unsigned long long) * ctx->max_sessions, st));
+    return 0;
+}
+
 int check_n(uint64_t n)
 {
     return n > 0x7fffffffull ? -EINVAL : 0;
@@ -2449,7 +2460,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     Workspace &w = ctx->ws;
     void *ptrs[] = {w.hot, w.pw, w.fin, w.powtab, w.acc, w.cnt, w.nch, w.chunk_end, w.v, w.excl, w.v_s,
                     w.excl_s, w.iota, w.perm, w.keys_s, w.last, w.list_frame, w.post, w.psnap, w.blockmax, w.zs,
-                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, w.rt, w.nonce, w.stage, ctx->sessions, ctx->peer, ctx->send, ctx->dbuf};
+                    w.lb_flag, w.lb_agg, w.lb_inc, w.temp, w.rt, w.nonce, w.stage, ctx->sessions, ctx->peer, ctx->send, ctx->zero_peer, ctx->dbuf};
     for (void *p : ptrs)
         if (p)
             (void) hipFree(p);
@@ -2715,7 +2726,12 @@ static int check_opts(const zmqg_batch_opts *o)
 
 static uint64_t opt_out_bytes(const zmqg_batch_opts *o)
 {
-    return o && o->size >= sizeof(zmqg_batch_opts) ? o->out_bytes : 0;
+    return o && o->size >= offsetof(zmqg_batch_opts, out_bytes) + sizeof(uint64_t) ? o->out_bytes : 0;
+}
+
+static const int32_t *opt_verdict_in(const zmqg_batch_opts *o)
+{
+    return o && o->size >= offsetof(zmqg_batch_opts, verdict_in) + sizeof(void *) ? o->verdict_in : nullptr;
 }
 
 // ZMQG_OPT_VERIFY_FIRST: frame i's payload, decoded into the staging area at
@@ -2724,14 +2740,30 @@ static uint64_t opt_out_bytes(const zmqg_batch_opts *o)
 // failed; a frame the decode left as it was (above the bound, or shorter
 // than the 33-byte MESSAGE minimum) is left as it was here too.  One
 // workgroup per frame; 16-byte stores in the aligned middle.
+// ZMQG_OPT_REPLAY_HOST: `verdict` (the host's header / replay verdict per
+// frame) comes first; the kernels' status stands only where it is 0, and a
+// frame it fails gets that status and flags 0.
 __global__ __launch_bounds__(256) void k_verify_copy(uint32_t n, const uint8_t *__restrict__ stage,
                                                      uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off,
                                                      const uint32_t *__restrict__ wire_len,
-                                                     const int32_t *__restrict__ status)
+                                                     int32_t *__restrict__ status,
+                                                     const int32_t *__restrict__ verdict,
+                                                     uint8_t *__restrict__ flags_out)
 {
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t wl = wire_len[i];
-        const int32_t stt = status[i];
+        int32_t stt = status[i];
+        if (verdict) {
+            const int32_t vd = verdict[i];
+            if (vd != 0 && stt != ZMQG_ERR_BOUND && stt != ZMQG_ERR_SESSION) {
+                __syncthreads(); // (every thread has read status[i])
+                if (threadIdx.x == 0) {
+                    status[i] = vd;
+                    flags_out[i] = 0;
+                }
+                stt = vd;
+            }
+        }
         if (wl <= 33u || stt == ZMQG_ERR_BOUND)
             continue;
         const uint64_t L = wl - 33u, o = out_off[i];
@@ -2833,6 +2865,11 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     if (!sid || !in_off || !wire_len || !in || !out_off || !out || !flags_out || !status_out)
         return -EINVAL;
     const bool verify_first = opts && (opts->flags & ZMQG_OPT_VERIFY_FIRST);
+    // the host applied the header and replay rules (opts->verdict_in)
+    const bool replay_host = opts && (opts->flags & ZMQG_OPT_REPLAY_HOST);
+    const int32_t *verdict = replay_host ? opt_verdict_in(opts) : nullptr;
+    if (replay_host && (!verify_first || !verdict || zres))
+        return -EINVAL;
     // (out_bytes may be 0 under VERIFY_FIRST: a batch of frames with no
     // payload bytes -- empty or under the 33-byte minimum -- stages nothing,
     // and each such frame still gets its own status)
@@ -2859,7 +2896,9 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     }
     const uint32_t nn = (uint32_t) n;
     int G = lanes_per_frame(ctx, nn);
-    const bool multi = ctx->sort_bits > 0;
+    // several sessions: the replay tables after the frame kernel; the host's
+    // verdicts need neither those nor the one-session look-back
+    const bool multi = ctx->sort_bits > 0 && !replay_host;
     FrameCtl ctl{};
     ctl.post = w.post;
     unsigned long long *smax = nullptr;
@@ -2877,7 +2916,17 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     rp.vout = w.v;
     rp.psnap = w.psnap;
     rp.peer = ctx->peer;
-    if (multi) {
+    if (replay_host) {
+        // the frame kernels' peer-nonce snapshot reads zeros (the device
+        // table is the host's to keep), and the big-frame finisher's replay
+        // prefix is zero: their replay test passes every header-valid frame
+        // and k_verify_copy applies the host's verdict over it
+        if ((rc = ensure_zero_peer(ctx, st)))
+            return rc;
+        rp.peer = ctx->zero_peer;
+        if (!ctl.no_body)
+            ZCHECK(ctx, hipMemsetAsync(w.excl, 0, sizeof(unsigned long long) * nn, st));
+    } else if (multi) {
         if (ctx->max_sessions > kReplayMaxSessions)
             rp.iota = w.iota; // (the sort fallback's values)
         if (smax)
@@ -2927,7 +2976,7 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     if (verify_first) {
         const uint32_t g = nn < 65536u ? nn : 65536u;
         hipLaunchKernelGGL(k_verify_copy, dim3(g), dim3(256), 0, st, nn, (const uint8_t *) out, out_user, out_off,
-                           wire_len, (const int32_t *) status_out);
+                           wire_len, status_out, verdict, flags_out);
         ZCHECK(ctx, hipGetLastError());
     }
     call.end();

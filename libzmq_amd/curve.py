@@ -65,11 +65,12 @@ _lib.zmqg_encode_batch.argtypes = [_P, _U64] + [_P] * 9
 _lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
 OPT_NONCE_AUTO = 1  # zmqg_batch_opts.flags: encode nonces from the sessions' send counters
 OPT_VERIFY_FIRST = 2  # zmqg_batch_opts.flags: decode writes out only after each frame's verdict
+OPT_REPLAY_HOST = 4  # zmqg_batch_opts.flags: the caller applied the header / replay rules (verdict_in)
 
 
 class BatchOpts(ctypes.Structure):  # zmqg_batch_opts
     _fields_ = [("size", _U32), ("flags", _U32), ("max_len", _U64), ("status_out", _P),
-                ("session_max_out", _P), ("out_bytes", _U64)]
+                ("session_max_out", _P), ("out_bytes", _U64), ("verdict_in", _P)]
 
 
 _lib.zmqg_encode_batch_ex.argtypes = [_P, _U64] + [_P] * 8 + [ctypes.POINTER(BatchOpts), _P]
@@ -240,12 +241,15 @@ class CurveContext:
     # max_len / status_out / session_max_out: zmqg_batch_opts (the _ex calls)
     # nonce_auto: encode takes nonces from the sessions' send counters (nonce may be None)
     @staticmethod
-    def _opts(max_len, status_out, session_max_out, nonce_auto=False, verify_first=False, out_bytes=0):
-        if not max_len and status_out is None and session_max_out is None and not nonce_auto and not verify_first:
+    def _opts(max_len, status_out, session_max_out, nonce_auto=False, verify_first=False, out_bytes=0,
+              verdict_in=None):
+        if (not max_len and status_out is None and session_max_out is None and not nonce_auto and not verify_first
+                and verdict_in is None):
             return None
-        fl = (OPT_NONCE_AUTO if nonce_auto else 0) | (OPT_VERIFY_FIRST if verify_first else 0)
+        fl = ((OPT_NONCE_AUTO if nonce_auto else 0) | (OPT_VERIFY_FIRST if verify_first else 0)
+              | (OPT_REPLAY_HOST if verdict_in is not None else 0))
         o = BatchOpts(ctypes.sizeof(BatchOpts), fl, int(max_len or 0), _ptr(status_out), _ptr(session_max_out),
-                      int(out_bytes))
+                      int(out_bytes), _ptr(verdict_in))
         return ctypes.byref(o), o
 
     def encode_batch(self, sid, nonce, flags, in_off, length, inp, out_off, out, stream=None, max_len=0,
@@ -257,16 +261,18 @@ class CurveContext:
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_encode_batch")
 
     def decode_batch(self, sid, in_off, wire_len, inp, out_off, out, flags_out, status_out, stream=None, max_len=0,
-                     session_max_out=None, verify_first=False, out_bytes=None):
+                     session_max_out=None, verify_first=False, out_bytes=None, verdict_in=None):
         """session_max_out: int64 tensor of max_sessions entries (device),
         receives each session's largest header-valid nonce of the batch.
         verify_first: ZMQG_OPT_VERIFY_FIRST (out receives only verified
         payloads and zeros; out's extent is taken from the tensor unless
-        out_bytes is given)."""
+        out_bytes is given).  verdict_in: int32 tensor (device) of the host's
+        header / replay verdicts, ZMQG_OPT_REPLAY_HOST (with verify_first)."""
         n = int(sid.numel())
         if out_bytes is None:
             out_bytes = out.numel() * out.element_size() if verify_first else 0
-        o = self._opts(max_len, None, session_max_out, verify_first=verify_first, out_bytes=out_bytes)
+        o = self._opts(max_len, None, session_max_out, verify_first=verify_first, out_bytes=out_bytes,
+                       verdict_in=verdict_in)
         self._check(_lib.zmqg_decode_batch_ex(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
                                               _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_decode_batch")

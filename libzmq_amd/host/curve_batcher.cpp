@@ -61,7 +61,8 @@ int curve_batcher_t::init ()
                  o_out_off = align256 (o_len + 4 * m),
                  o_flags_out = align256 (o_out_off + 8 * m),
                  o_status = align256 (o_flags_out + m),
-                 o_in = align256 (o_status + 4 * m),
+                 o_verdict = align256 (o_status + 4 * m),
+                 o_in = align256 (o_verdict + 4 * m),
                  o_out = align256 (o_in + _config.slot_bytes),
                  total = align256 (o_out + _out_cap);
     _slots.resize (_config.slots);
@@ -83,6 +84,7 @@ int curve_batcher_t::init ()
         s.out_off = reinterpret_cast<uint64_t *> (b + o_out_off);
         s.flags_out = b + o_flags_out;
         s.status = reinterpret_cast<int32_t *> (b + o_status);
+        s.verdict = reinterpret_cast<int32_t *> (b + o_verdict);
         s.in = b + o_in;
         s.out = b + o_out;
         s.tags.resize (m);
@@ -194,6 +196,16 @@ int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
         errno = EIO;
         return -1;
     }
+    uint64_t *peer = NULL;
+    if (_config.replay_host && _config.verify_first
+        && conn_->host_peer (&peer) != 0) {
+        errno = EIO;
+        return -1;
+    }
+    if (!peer && conn_->device_peer () != 0) {
+        errno = EIO;
+        return -1;
+    }
     //  decoded in place: each payload byte is left over its own ciphertext
     //  byte, at wire offset 33 of the frame, so a decode slot needs no output
     //  area (the reference decrypts into message + 16 instead,
@@ -207,6 +219,14 @@ int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
     s->len[i] = static_cast<uint32_t> (size_);
     s->out_off[i] = s->in_used + 33;
     s->tags[i] = tag_;
+    if (peer) {
+        //  the connection's frames reach this call in receive order
+        s->verdict[i] =
+          curve_encoding_gpu_t::frame_verdict (wire_, size_, peer);
+        if (s->verdict[i] == 0)
+            conn_->_peer_state = curve_encoding_gpu_t::peer_host_ahead;
+    } else
+        conn_->_peer_state = curve_encoding_gpu_t::peer_device_ahead;
     if (size_ > s->max_len)
         s->max_len = size_;
     if (size_)
@@ -234,6 +254,10 @@ int curve_batcher_t::launch (slot_t *s)
         //  runs: verify before any plaintext reaches it, as libsodium's open
         //  does (src/curve_mechanism_base.cpp:226-228)
         o.flags = _config.verify_first ? ZMQG_OPT_VERIFY_FIRST : 0;
+        if (_config.verify_first && _config.replay_host) {
+            o.flags |= ZMQG_OPT_REPLAY_HOST;
+            o.verdict_in = s->verdict;
+        }
         o.out_bytes = s->in_used;
         rc = zmqg_decode_batch_ex (_ctx, s->n, s->sid, s->in_off, s->len,
                                    s->in, s->out_off, s->in, s->flags_out,

@@ -83,6 +83,12 @@ class curve_batcher_t
         //  receive slots decoded with ZMQG_OPT_VERIFY_FIRST: the pinned slot
         //  never holds plaintext of a frame that fails (default on)
         bool verify_first;
+        //  receive slots carry the host's header / replay verdict per frame
+        //  (ZMQG_OPT_REPLAY_HOST, with verify_first): the batcher sees each
+        //  connection's frames in order and applies check_validity's rules
+        //  itself, so the device only authenticates and opens (two kernel
+        //  launches a batch instead of seven).  Default on.
+        bool replay_host;
         //  >= 0: every launched slot's fence also writes this eventfd when
         //  the stream reaches it (zmqg_fence_record_notify), so a poller
         //  sleeping on it wakes for the completion.  -1: fences only.
@@ -92,6 +98,7 @@ class curve_batcher_t
             slot_bytes (8u << 20),
             slots (4),
             verify_first (true),
+            replay_host (true),
             notify_fd (-1)
         {
         }
@@ -154,6 +161,7 @@ class curve_batcher_t
         uint64_t *out_off;
         uint8_t *flags_out;
         int32_t *status;
+        int32_t *verdict; //  decode: the host's verdict (replay_host)
         uint8_t *in;
         uint8_t *out;
         std::vector<uint64_t> tags;

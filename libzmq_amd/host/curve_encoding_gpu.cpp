@@ -82,7 +82,9 @@ curve_encoding_gpu_t::curve_encoding_gpu_t (zmqg_ctx *ctx_,
     _sid (sid_),
     _cn_nonce (1), // src/curve_mechanism_base.cpp:20-21
     _installed (false),
-    _downgrade_sub (downgrade_sub_)
+    _downgrade_sub (downgrade_sub_),
+    _peer (1), // src/curve_mechanism_base.cpp:21
+    _peer_state (peer_synced)
 {
     memcpy (_encode_nonce_prefix, encode_nonce_prefix_, 16);
     memcpy (_decode_nonce_prefix, decode_nonce_prefix_, 16);
@@ -97,25 +99,76 @@ int curve_encoding_gpu_t::sync_session ()
         return 0;
     //  the reference's _cn_peer_nonce starts at 1 (curve_mechanism_base.cpp:21)
     uint64_t peer = 1;
-    if (_installed && zmqg_session_get_peer_nonce (_ctx, _sid, &peer) != 0)
-        return -1;
+    if (_installed) {
+        uint64_t *p;
+        if (host_peer (&p) != 0)
+            return -1;
+        peer = *p;
+    }
     if (zmqg_session_set (_ctx, _sid, _cn_precom, _encode_nonce_prefix,
                           _decode_nonce_prefix, _downgrade_sub ? 1 : 0, peer)
         != 0)
         return -1;
     memcpy (_installed_precom, _cn_precom, sizeof _cn_precom);
     _installed = true;
+    _peer = peer;
+    _peer_state = peer_synced;
+    return 0;
+}
+
+int curve_encoding_gpu_t::host_peer (uint64_t **peer_)
+{
+    if (_peer_state == peer_device_ahead) {
+        if (zmqg_session_get_peer_nonce (_ctx, _sid, &_peer) != 0)
+            return -1;
+        _peer_state = peer_synced;
+    }
+    *peer_ = &_peer;
+    return 0;
+}
+
+int curve_encoding_gpu_t::device_peer ()
+{
+    if (_peer_state == peer_host_ahead) {
+        if (zmqg_session_set_peer_nonce (_ctx, _sid, _peer) != 0)
+            return -1;
+        _peer_state = peer_synced;
+    }
+    return 0;
+}
+
+int32_t curve_encoding_gpu_t::frame_verdict (const uint8_t *wire_,
+                                             size_t size_,
+                                             uint64_t *peer_)
+{
+    if (size_ <= 1 || size_ <= wire_[0])
+        return ZMQG_ERR_MALFORMED_UNSPECIFIED; //  src/mechanism_base.cpp:16-22
+    if (size_ < 8 || memcmp (wire_, "\x07MESSAGE", 8) != 0)
+        return ZMQG_ERR_UNEXPECTED_COMMAND; //  src/curve_mechanism_base.cpp:85-90
+    if (size_ < 33)
+        return ZMQG_ERR_MALFORMED_MESSAGE; //  :92-96
+    uint64_t nonce = 0;
+    for (int k = 0; k < 8; ++k)
+        nonce = nonce << 8 | wire_[8 + k]; //  get_uint64: big-endian
+    if (nonce <= *peer_)
+        return ZMQG_ERR_INVALID_SEQUENCE; //  :99-104
+    *peer_ = nonce; //  :105, before the MAC
     return 0;
 }
 
 void curve_encoding_gpu_t::set_peer_nonce (nonce_t peer_nonce_)
 {
-    if (sync_session () == 0)
-        zmqg_session_set_peer_nonce (_ctx, _sid, peer_nonce_);
+    if (sync_session () == 0
+        && zmqg_session_set_peer_nonce (_ctx, _sid, peer_nonce_) == 0) {
+        _peer = peer_nonce_;
+        _peer_state = peer_synced;
+    }
 }
 
 curve_encoding_gpu_t::nonce_t curve_encoding_gpu_t::get_peer_nonce () const
 {
+    if (_peer_state == peer_host_ahead)
+        return _peer;
     uint64_t p = 0;
     zmqg_session_get_peer_nonce (_ctx, _sid, &p);
     return p;
@@ -154,17 +207,23 @@ int curve_encoding_gpu_t::decode_msg (const uint8_t *in_,
         errno = EINVAL;
         return -1;
     }
-    if (sync_session () != 0) {
+    if (sync_session () != 0 || device_peer () != 0) {
         errno = EIO;
         return -1;
     }
+    //  the host copy follows the device's through the same rule
+    uint64_t peer = _peer;
+    if (_peer_state == peer_synced)
+        frame_verdict (in_, wire_len_, &peer);
     int32_t status = 0;
     const int rc = zmqg_decode_msg (_ctx, _sid, in_, (uint32_t) wire_len_, out_,
                                     flags_out_, &status);
     if (rc != 0) {
         errno = -rc;
+        _peer_state = peer_device_ahead;
         return -1;
     }
+    _peer = peer;
     if (status != 0) {
         //  src/curve_mechanism_base.cpp:84-108, 277-281
         if (error_event_code_)
@@ -266,10 +325,11 @@ int curve_encoding_gpu_t::decode_many (curve_encoding_gpu_t *const *dec_,
             errno = EINVAL;
             return -1;
         }
-        if (d->sync_session () != 0) {
+        if (d->sync_session () != 0 || d->device_peer () != 0) {
             errno = EIO;
             return -1;
         }
+        d->_peer_state = peer_device_ahead; //  the call advances the device's
         sid[i] = d->_sid;
         wire_len[i] = (uint32_t) msgs_[i]->size ();
         in_off[i] = in_bytes;

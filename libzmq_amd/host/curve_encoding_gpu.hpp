@@ -125,11 +125,37 @@ class curve_encoding_gpu_t
     void set_peer_nonce (nonce_t peer_nonce_);
     nonce_t get_peer_nonce () const;
 
+    //  The header rules and the replay rule of one received frame, in
+    //  order, on the host: check_basic_command_structure
+    //  (src/mechanism_base.cpp:14-25) and check_validity
+    //  (src/curve_mechanism_base.cpp:80-106).  0, or the
+    //  ZMQ_PROTOCOL_ERROR_ZMTP_* code; *peer_ advances before the MAC, as
+    //  set_peer_nonce does there.
+    static int32_t frame_verdict (const uint8_t *wire_,
+                                  size_t size_,
+                                  uint64_t *peer_);
+
   private:
     friend class curve_batcher_t;
 
     //  installs the session on the device when the precom buffer changed
     int sync_session ();
+
+    //  The connection's peer nonce.  The device's copy is advanced by the
+    //  calls that apply the replay rule there (decode_msg, decode_many); a
+    //  batch under ZMQG_OPT_REPLAY_HOST (curve_batcher_t) advances the host's
+    //  copy instead.  Each side catches up from the other before it is used.
+    enum peer_state_t
+    {
+        peer_synced,      //  _peer == the device's
+        peer_host_ahead,  //  _peer is newer: set the device's before use
+        peer_device_ahead //  the device's is newer: read it before use
+    };
+    //  the host copy, current (reads the device's when that is ahead);
+    //  -1 when the device cannot be read
+    int host_peer (uint64_t **peer_);
+    //  the device copy, current (writes _peer when the host is ahead)
+    int device_peer ();
 
     zmqg_ctx *const _ctx;
     const uint32_t _sid;
@@ -140,6 +166,8 @@ class curve_encoding_gpu_t
     uint8_t _installed_precom[32];
     bool _installed;
     const bool _downgrade_sub;
+    uint64_t _peer;
+    peer_state_t _peer_state;
 
     curve_encoding_gpu_t (const curve_encoding_gpu_t &);
     curve_encoding_gpu_t &operator= (const curve_encoding_gpu_t &);

@@ -113,6 +113,8 @@ class curve_io_hook_t : private curve_sink_t
     //  launch and wait for everything queued (shutdown, tests)
     int drain ();
     size_t outstanding () const;
+    //  messages launched and not yet delivered
+    size_t in_flight () const { return _batcher.in_flight (); }
     //  launched batches whose results have not been delivered yet (a poller
     //  that holds new messages back while the device is busy uses it)
     size_t batches_in_flight () const { return _batcher.batches_in_flight (); }

@@ -6,6 +6,7 @@
 
 #include <errno.h>
 #include <poll.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -81,8 +82,12 @@ class curve_io_poll_t : public i_poll_events
     //  i_poll_events: the eventfd (batches came back) and the flush timer
     void in_event ()
     {
+        const uint64_t t0 = stats_ns ();
         const int rc = _hook->in_event ();
         errno_assert (rc >= 0);
+        ++_wakes;
+        _delivered += rc;
+        _deliver_ns += stats_ns () - t0;
         launch_if_idle ();
     }
     void out_event () { zmq_assert (false); }
@@ -95,6 +100,16 @@ class curve_io_poll_t : public i_poll_events
     ~curve_io_poll_t ()
     {
         //  the thread is exiting: its poller no longer runs this object
+        if (getenv ("ZMQG_ENGINE_STATS"))
+            fprintf (stderr,
+                     "zmqg engine: %llu wake-ups, %llu launches, %llu "
+                     "messages launched, %llu delivered by wake-ups, "
+                     "%.3f ms in launches, %.3f ms in deliveries\n",
+                     (unsigned long long) _wakes,
+                     (unsigned long long) _launches,
+                     (unsigned long long) _launched,
+                     (unsigned long long) _delivered, _launch_ns * 1e-6,
+                     _deliver_ns * 1e-6);
         delete _hook;
     }
 
@@ -110,7 +125,14 @@ class curve_io_poll_t : public i_poll_events
         _handle (static_cast<poller_t::handle_t> (NULL)),
         _users (0),
         _timer (false),
-        _max_flight (env_size ("ZMQG_ENGINE_FLIGHT", 2))
+        _max_flight (env_size ("ZMQG_ENGINE_FLIGHT", 2)),
+        _wakes (0),
+        _launches (0),
+        _launched (0),
+        _delivered (0),
+        _launch_ns (0),
+        _deliver_ns (0),
+        _stats (getenv ("ZMQG_ENGINE_STATS") != NULL)
     {
         _config.slots = static_cast<int> (env_size ("ZMQG_ENGINE_SLOTS", 6));
         _config.slot_msgs = env_size ("ZMQG_ENGINE_SLOT_MSGS", 8192);
@@ -134,8 +156,12 @@ class curve_io_poll_t : public i_poll_events
         if (!_hook->flush_pending ()
             || _hook->batches_in_flight () >= _max_flight)
             return;
+        ++_launches;
+        _launched += _hook->outstanding () - _hook->in_flight ();
+        const uint64_t t0 = stats_ns ();
         const int rc = _hook->timer_event ();
         errno_assert (rc == 0);
+        _launch_ns += stats_ns () - t0;
     }
 
     poller_t *const _poller;
@@ -145,6 +171,17 @@ class curve_io_poll_t : public i_poll_events
     int _users;
     bool _timer;
     const size_t _max_flight;
+    //  ZMQG_ENGINE_STATS: printed when the thread exits
+    uint64_t _wakes, _launches, _launched, _delivered, _launch_ns, _deliver_ns;
+    const bool _stats;
+    uint64_t stats_ns () const
+    {
+        if (!_stats)
+            return 0;
+        timespec t;
+        clock_gettime (CLOCK_MONOTONIC, &t);
+        return static_cast<uint64_t> (t.tv_sec) * 1000000000u + t.tv_nsec;
+    }
 
     struct holder_t
     {

@@ -16,10 +16,12 @@
 #          to the I/O thread's batched codec (libzmq_amd/host/zmq_curve_engine.cpp,
 #          curve_engine_hook.cpp, curve_batcher.cpp), whose eventfd sits in the
 #          thread's poller.
-# Every copy also carries tests/host/libzmq_zmtp30_test.patch: a test-only
-# switch (ZMQG_TEST_ZMTP30 in the environment; unset, the library behaves as
-# the reference) that makes the side announce ZMTP 3.0, so its peer runs
-# handshake_v3_0 with downgrade_sub.
+# Every copy also carries tests/host/libzmq_test_switches.patch, test-only
+# switches read from the environment (unset, the library behaves as the
+# reference): ZMQG_TEST_ZMTP30 makes the side announce ZMTP 3.0, so its peer
+# runs handshake_v3_0 with downgrade_sub (ZMQG_TEST_ZMTP30_TRACE reports it);
+# INTEROP_PROFILE leaves SIGPROF unblocked in libzmq's threads for the test
+# program's sampling profiler.
 # The reference's own build system is not run: g++ on its sources, in scratch
 # copies outside the repository, with the test-only
 # tests/host/ref_platform_full/platform.hpp in place of the generated one;
@@ -105,14 +107,14 @@ link () {
     "$OUT/$name/libzmq.so.5" -Wl,-rpath,'$ORIGIN/'"$name" -lpthread
 }
 
-variant stock "" libzmq_zmtp30_test.patch
+variant stock "" libzmq_test_switches.patch
 link stock
 
-variant zmqg "-DZMQ_USE_ZMQG_CURVE" libzmq_zmtp30_test.patch libzmq_zmqg.patch
+variant zmqg "-DZMQ_USE_ZMQG_CURVE" libzmq_test_switches.patch libzmq_zmqg.patch
 link zmqg curve_encoding_gpu.cpp
 
 variant zmqgb "-DZMQ_USE_ZMQG_CURVE -DZMQ_USE_ZMQG_CURVE_BATCHED" \
-  libzmq_zmtp30_test.patch libzmq_zmqg.patch libzmq_zmqg_batched.patch
+  libzmq_test_switches.patch libzmq_zmqg.patch libzmq_zmqg_batched.patch
 link zmqgb curve_encoding_gpu.cpp curve_batcher.cpp curve_engine_hook.cpp zmq_curve_engine.cpp
 
 echo "build_libzmq: $OUT/interop_stock $OUT/interop_zmqg $OUT/interop_zmqgb"

@@ -256,51 +256,71 @@ int main (int argc, char **argv)
         }
     }
     const int n_in = (int) in_wire.size ();
-    for (int c = 0; c < n_conn; ++c) {
-        a.server[c]->set_peer_nonce (0);
-        b.server[c]->set_peer_nonce (0);
-    }
-    sink_t dsink;
-    zmqg::curve_batcher_t *dbp = new zmqg::curve_batcher_t (a.ctx, &dsink, cfg);
-    zmqg::curve_batcher_t &dbatcher = *dbp;
-    CHECK (dbatcher.init () == 0);
-    for (int k = 0; k < n_in; ++k) {
-        const uint8_t *p = in_wire[k].empty () ? NULL : &in_wire[k][0];
-        CHECK (dbatcher.submit_decode (a.server[in_conn[k]], p, in_wire[k].size (), (uint64_t) k) == 0);
-        if (k % 131 == 130)
-            CHECK (dbatcher.flush () == 0);
-        CHECK (dbatcher.poll () >= 0);
-    }
-    CHECK (dbatcher.drain () >= 0);
-    CHECK ((int) dsink.order.size () == n_in);
-    delete dbp;
-    int failures = 0;
-    for (int k = 0; k < n_in; ++k) {
-        zmqg::msg_buf_t msg;
-        msg.bytes = in_wire[k];
-        int code = 0;
-        const int rc = b.server[in_conn[k]]->decode (&msg, &code);
-        const result_t &r = dsink.got[k];
-        if (rc == 0) {
-            CHECK (r.status == 0);
-            CHECK (r.bytes == msg.bytes);
-            CHECK (r.flags == msg.flags);
-        } else {
-            CHECK (r.status == code && code != 0);
-            ++failures;
+    //  twice: with the host applying the header / replay rules
+    //  (ZMQG_OPT_REPLAY_HOST, the default) and with the device applying them
+    for (int pass = 0; pass < 2; ++pass) {
+        zmqg::curve_batcher_t::config_t dcfg = cfg;
+        dcfg.replay_host = pass == 0;
+        for (int c = 0; c < n_conn; ++c) {
+            a.server[c]->set_peer_nonce (0);
+            b.server[c]->set_peer_nonce (0);
         }
-        const int cmd_type = in_src[k] >= 0 ? mflags[in_src[k]] & 28 : 0; // msg_t CMD_TYPE_MASK
-        if (in_src[k] >= 0 && cmd_type != ZMQG_MSG_SUBSCRIBE && cmd_type != ZMQG_MSG_CANCEL) {
-            // plain messages come back as they went in (sub/cancel carry
-            // their command name, src/curve_mechanism_base.cpp:143-159)
-            const int m = in_src[k];
-            CHECK (r.status == 0 && r.bytes == payload[m]);
-            CHECK (r.flags == (mflags[m] & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND)));
+        sink_t dsink;
+        zmqg::curve_batcher_t *dbp = new zmqg::curve_batcher_t (a.ctx, &dsink, dcfg);
+        zmqg::curve_batcher_t &dbatcher = *dbp;
+        CHECK (dbatcher.init () == 0);
+        for (int k = 0; k < n_in; ++k) {
+            const uint8_t *p = in_wire[k].empty () ? NULL : &in_wire[k][0];
+            CHECK (dbatcher.submit_decode (a.server[in_conn[k]], p, in_wire[k].size (), (uint64_t) k) == 0);
+            if (k % 131 == 130)
+                CHECK (dbatcher.flush () == 0);
+            CHECK (dbatcher.poll () >= 0);
+        }
+        CHECK (dbatcher.drain () >= 0);
+        CHECK ((int) dsink.order.size () == n_in);
+        delete dbp;
+        int failures = 0;
+        for (int k = 0; k < n_in; ++k) {
+            zmqg::msg_buf_t msg;
+            msg.bytes = in_wire[k];
+            int code = 0;
+            const int rc = b.server[in_conn[k]]->decode (&msg, &code);
+            const result_t &r = dsink.got[k];
+            if (rc == 0) {
+                CHECK (r.status == 0);
+                CHECK (r.bytes == msg.bytes);
+                CHECK (r.flags == msg.flags);
+            } else {
+                CHECK (r.status == code && code != 0);
+                ++failures;
+            }
+            const int cmd_type = in_src[k] >= 0 ? mflags[in_src[k]] & 28 : 0; // msg_t CMD_TYPE_MASK
+            if (in_src[k] >= 0 && cmd_type != ZMQG_MSG_SUBSCRIBE && cmd_type != ZMQG_MSG_CANCEL) {
+                // plain messages come back as they went in (sub/cancel carry
+                // their command name, src/curve_mechanism_base.cpp:143-159)
+                const int m = in_src[k];
+                CHECK (r.status == 0 && r.bytes == payload[m]);
+                CHECK (r.flags == (mflags[m] & (ZMQG_MSG_MORE | ZMQG_MSG_COMMAND)));
+            }
+        }
+        CHECK (failures > 0);
+        for (int c = 0; c < n_conn; ++c)
+            CHECK (a.server[c]->get_peer_nonce () == b.server[c]->get_peer_nonce ());
+        if (pass == 0) {
+            //  the host's peer nonces reach the device before a per-message
+            //  decode: a replay of each connection's last frame fails there
+            //  as it failed in the batch
+            for (int k = n_in - 1, done = 0; k >= 0 && done < 4; --k) {
+                if (in_src[k] < 0)
+                    continue;
+                zmqg::msg_buf_t msg;
+                msg.bytes = in_wire[k];
+                int code = 0;
+                CHECK (a.server[in_conn[k]]->decode (&msg, &code) == -1 && code == ZMQG_ERR_INVALID_SEQUENCE);
+                ++done;
+            }
         }
     }
-    CHECK (failures > 0);
-    for (int c = 0; c < n_conn; ++c)
-        CHECK (a.server[c]->get_peer_nonce () == b.server[c]->get_peer_nonce ());
 
     {   //  receive slots holding no payload bytes at all (in_used == 0:
         //  empty frames) and frames under the 33-byte MESSAGE minimum: each

@@ -52,6 +52,17 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <cxxabi.h>
+#include <dirent.h>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <pthread.h>
+#include <signal.h>
+#include <sys/syscall.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
 #include <vector>
 
 static const char server_public[] = "rq:rM>}U?@Lns47E1%kR.o@n%FcmmsL/@{H8]yf7";
@@ -107,6 +118,189 @@ static double now_s ()
     timespec t;
     clock_gettime (CLOCK_MONOTONIC, &t);
     return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+//  CPU seconds used so far by each thread of this process, by thread name
+//  (/proc/self/task/*/stat: comm, utime, stime); INTEROP_THREAD_CPU set in
+//  the environment makes both sides print the split of the timed window
+//  to stderr ("cpu <thread> <seconds>"), to tell which thread bounds a rate.
+typedef std::map<std::string, double> cpu_map_t;
+static cpu_map_t thread_cpu ()
+{
+    cpu_map_t m;
+    DIR *d = opendir ("/proc/self/task");
+    if (!d)
+        return m;
+    const double tick = (double) sysconf (_SC_CLK_TCK);
+    while (dirent *e = readdir (d)) {
+        if (e->d_name[0] == '.')
+            continue;
+        char path[300], buf[1024];
+        snprintf (path, sizeof path, "/proc/self/task/%s/stat", e->d_name);
+        FILE *f = fopen (path, "r");
+        if (!f)
+            continue;
+        const size_t n = fread (buf, 1, sizeof buf - 1, f);
+        fclose (f);
+        buf[n] = 0;
+        char *l = strchr (buf, '('), *r = strrchr (buf, ')');
+        if (!l || !r)
+            continue;
+        //  by name and thread id: threads a library starts from an I/O
+        //  thread inherit its name (the HIP runtime's do)
+        const std::string name = std::string (l + 1, r) + "#" + e->d_name;
+        //  after ") ": state, then fields 4.. ; utime and stime are 14, 15
+        unsigned long long ut = 0, st = 0;
+        const char *q = r + 2;
+        for (int field = 3; field < 14 && q; ++field) {
+            q = strchr (q, ' ');
+            if (q)
+                ++q;
+        }
+        if (q && sscanf (q, "%llu %llu", &ut, &st) == 2)
+            m[name] += (ut + st) / tick;
+    }
+    closedir (d);
+    return m;
+}
+
+static void print_cpu (const cpu_map_t &a_, const cpu_map_t &b_, double wall_)
+{
+    if (!getenv ("INTEROP_THREAD_CPU"))
+        return;
+    for (cpu_map_t::const_iterator it = b_.begin (); it != b_.end (); ++it) {
+        cpu_map_t::const_iterator p = a_.find (it->first);
+        const double d = it->second - (p == a_.end () ? 0.0 : p->second);
+        if (d > 0)
+            fprintf (stderr, "cpu %s %.3f of %.3f s\n", it->first.c_str (), d, wall_);
+    }
+}
+
+//  INTEROP_PROFILE set: a sampling profile of the threads named ZMQbg/IO/0
+//  (the I/O thread, and threads it started) over the timed window -- a
+//  sampler thread sends SIGPROF every 200 us, the handler records the stack
+//  (backtrace), and stop () prints the functions seen most often on top of
+//  the stack ("self") and anywhere in it ("incl"), per thread, to stderr.
+//  A diagnostic of where the I/O thread's time goes; no effect otherwise.
+namespace sampler
+{
+const int depth = 32;
+const size_t cap = 60000;
+static void *frames[cap][depth];
+static int nframes[cap], owner[cap];
+static volatile size_t count;
+static volatile int active, stopping;
+static std::vector<pid_t> targets;
+static pthread_t thread;
+
+static void on_signal (int)
+{
+    if (!active)
+        return;
+    const size_t i = __sync_fetch_and_add (&count, 1);
+    if (i >= cap)
+        return;
+    const pid_t me = (pid_t) syscall (SYS_gettid);
+    int k = 0;
+    while (k < (int) targets.size () && targets[k] != me)
+        ++k;
+    owner[i] = k;
+    nframes[i] = backtrace (frames[i], depth);
+}
+
+static void *loop (void *)
+{
+    while (!stopping) {
+        for (size_t k = 0; k < targets.size (); ++k)
+            syscall (SYS_tgkill, getpid (), targets[k], SIGPROF);
+        usleep (200);
+    }
+    return NULL;
+}
+
+static void start ()
+{
+    if (!getenv ("INTEROP_PROFILE"))
+        return;
+    void *warm[4];
+    backtrace (warm, 4); //  (loads libgcc before any signal arrives)
+    DIR *d = opendir ("/proc/self/task");
+    while (dirent *e = d ? readdir (d) : NULL) {
+        char path[300], name[64] = "";
+        snprintf (path, sizeof path, "/proc/self/task/%s/comm", e->d_name);
+        FILE *f = fopen (path, "r");
+        if (!f)
+            continue;
+        if (fgets (name, sizeof name, f) && strncmp (name, "ZMQbg/IO", 8) == 0)
+            targets.push_back ((pid_t) atoi (e->d_name));
+        fclose (f);
+    }
+    if (d)
+        closedir (d);
+    struct sigaction sa;
+    memset (&sa, 0, sizeof sa);
+    sa.sa_handler = on_signal;
+    sa.sa_flags = SA_RESTART;
+    sigaction (SIGPROF, &sa, NULL);
+    active = 1;
+    pthread_create (&thread, NULL, loop, NULL);
+}
+
+static std::string symbol (void *a_)
+{
+    Dl_info di;
+    if (!dladdr (a_, &di) || !di.dli_sname) {
+        char b[64];
+        snprintf (b, sizeof b, "%s+?", di.dli_fname ? strrchr (di.dli_fname, '/') + 1 : "?");
+        return b;
+    }
+    int st = 0;
+    char *dm = abi::__cxa_demangle (di.dli_sname, NULL, NULL, &st);
+    std::string r = st == 0 && dm ? dm : di.dli_sname;
+    free (dm);
+    const size_t paren = r.find ('(');
+    return paren == std::string::npos ? r : r.substr (0, paren);
+}
+
+static void stop ()
+{
+    if (!active)
+        return;
+    active = 0;
+    stopping = 1;
+    pthread_join (thread, NULL);
+    const size_t n = count < cap ? count : cap;
+    fprintf (stderr, "prof threads %zu samples %zu\n", targets.size (), (size_t) count);
+    for (size_t k = 0; k < targets.size (); ++k) {
+        std::map<std::string, int> self, incl;
+        int total = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (owner[i] != (int) k || nframes[i] <= 2)
+                continue;
+            ++total;
+            //  frames 0, 1: the handler and the signal trampoline
+            self[symbol (frames[i][2])]++;
+            std::map<std::string, int> seen;
+            for (int j = 2; j < nframes[i]; ++j)
+                seen[symbol (frames[i][j])] = 1;
+            for (std::map<std::string, int>::iterator it = seen.begin (); it != seen.end (); ++it)
+                incl[it->first]++;
+        }
+        if (!total)
+            continue;
+        for (int pass = 0; pass < 2; ++pass) {
+            std::map<std::string, int> &m = pass ? incl : self;
+            std::vector<std::pair<int, std::string> > v;
+            for (std::map<std::string, int>::iterator it = m.begin (); it != m.end (); ++it)
+                v.push_back (std::make_pair (-it->second, it->first));
+            std::sort (v.begin (), v.end ());
+            for (size_t i = 0; i < v.size () && i < (pass ? 45u : 30u); ++i)
+                fprintf (stderr, "prof %d %s %5.1f%% %s\n", (int) targets[k], pass ? "incl" : "self",
+                         -100.0 * v[i].first / total, v[i].second.c_str ());
+        }
+        fprintf (stderr, "prof %d samples %d\n", (int) targets[k], total);
+    }
+}
 }
 
 static void setup_heartbeats (void *s_, int ivl_)
@@ -300,6 +494,7 @@ int main (int argc, char **argv)
         CHECK (zmq_msg_init (&m) == 0);
         uint64_t frames = 0, bytes = 0;
         double t0 = 0;
+        cpu_map_t c0;
         for (uint64_t i = 0; i < n; ++i) {
             plan (seed, i, parts);
             for (size_t p = 0; p < parts.size (); ++p) {
@@ -309,8 +504,11 @@ int main (int argc, char **argv)
                              zmq_strerror (zmq_errno ()));
                     return 1;
                 }
-                if (i == 0 && p == 0)
+                if (i == 0 && p == 0) {
                     t0 = now_s ();
+                    c0 = thread_cpu ();
+                    sampler::start ();
+                }
                 const bool more = zmq_msg_more (&m) != 0;
                 if ((size_t) rc != parts[p].size () || more != (p + 1 < parts.size ())
                     || (rc && memcmp (zmq_msg_data (&m), &parts[p][0], rc) != 0)) {
@@ -323,6 +521,8 @@ int main (int argc, char **argv)
             }
         }
         const double dt = now_s () - t0;
+        sampler::stop ();
+        print_cpu (c0, thread_cpu (), dt);
         CHECK (zmq_msg_close (&m) == 0);
         //  the acknowledgement, as a CURVE client of the sender's process
         void *a = zmq_socket (ctx, ZMQ_PUSH);
@@ -355,7 +555,15 @@ int main (int argc, char **argv)
     CHECK (zmq_setsockopt (s, ZMQ_CURVE_SECRETKEY, client_secret, 40) == 0);
     setup_heartbeats (s, ivl);
     CHECK (zmq_connect (s, endpoint) == 0);
+    cpu_map_t c0;
+    double t0 = 0;
     for (uint64_t i = 0; i < n; ++i) {
+        if (i == 1) {
+            //  (after the first send, which waits for the handshake)
+            t0 = now_s ();
+            c0 = thread_cpu ();
+            sampler::start ();
+        }
         plan (seed, i, parts);
         for (size_t p = 0; p < parts.size (); ++p)
             CHECK (zmq_send (s, parts[p].empty () ? NULL : &parts[p][0], parts[p].size (),
@@ -368,6 +576,8 @@ int main (int argc, char **argv)
         fprintf (stderr, "FAIL: no acknowledgement (%d)\n", rc);
         return 1;
     }
+    sampler::stop ();
+    print_cpu (c0, thread_cpu (), now_s () - t0);
     CHECK (zmq_close (a) == 0);
     CHECK (zmq_close (s) == 0);
     CHECK (zmq_ctx_term (ctx) == 0);

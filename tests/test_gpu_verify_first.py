@@ -176,3 +176,91 @@ def test_verify_first_extent_checks(torch_cuda, C):
     assert stt[0] == 0 and stt[1] == 0
     assert stt[2] == C.ERR_BOUND and stt[3] == C.ERR_BOUND
     assert bool((o[int(pay_off[2]):] == 0x77).all())
+
+
+def _host_verdicts(wire, wire_off, wl, sid, peer):
+    """check_basic_command_structure + check_validity in frame order
+    (src/mechanism_base.cpp:14-25, src/curve_mechanism_base.cpp:80-106), the
+    rule ZMQG_OPT_REPLAY_HOST's caller applies; advances `peer` per session."""
+    v = np.zeros(len(wl), np.int32)
+    for i in range(len(wl)):
+        L, o = int(wl[i]), int(wire_off[i])
+        f = wire[o:o + L].tobytes()
+        if L <= 1 or L <= f[0]:
+            v[i] = 0x10000011
+        elif L < 8 or f[:8] != b"\x07MESSAGE":
+            v[i] = 0x10000001
+        elif L < 33:
+            v[i] = 0x10000012
+        else:
+            nonce = int.from_bytes(f[8:16], "big")
+            if nonce <= peer[sid[i]]:
+                v[i] = 0x10000002
+            else:
+                peer[sid[i]] = nonce
+    return v
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_replay_host_matches_oracle(torch_cuda, C, big):
+    """ZMQG_OPT_REPLAY_HOST: eight interleaved sessions with replays,
+    reordering, tampered tags, broken headers and short frames; the host's
+    verdicts plus the device's open give the oracle's statuses, flags and
+    payloads, and the device's peer nonces are left alone.  `big` adds
+    frames above the frame kernel's 4.5 KiB (the body kernels run)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(93)
+    S = 8
+    precoms = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(S)]
+    sess = O.make_sessions(precoms, dec_prefix=O.CLIENT_PREFIX)
+    choices = [0, 1, 31, 200, 1024, 4000] + ([9000, 70000] if big else [])
+    n = 600
+    sizes = [int(x) for x in rng.choice(choices, n)]
+    sid = rng.integers(0, S, n).astype(np.uint32)
+    nonce = np.zeros(n, np.uint64)
+    nxt = [5] * S
+    for i in range(n):
+        s = int(sid[i])
+        r = rng.random()
+        if r < 0.06 and nxt[s] > 6:
+            nonce[i] = nxt[s] - 1 - int(rng.integers(0, 2))  # a replay
+        else:
+            nonce[i] = nxt[s]
+            nxt[s] += 1 + int(rng.integers(0, 3))  # gaps are fine
+    payloads = [rng.integers(0, 256, s_, dtype=np.uint8).tobytes() for s_ in sizes]
+    inp, in_off = pack(payloads)
+    flags = (np.arange(n) % 3 == 0).astype(np.uint8)
+    wl = np.array([s_ + 33 for s_ in sizes], np.uint32)
+    wire_off = np.concatenate([[0], np.cumsum(wl)[:-1]]).astype(np.uint64)
+    enc = O.make_sessions(precoms)
+    wire = O.encode_batch(enc, sid, nonce, flags, in_off, np.array(sizes, np.uint32), inp, wire_off, int(wl.sum()))
+    for i in range(0, n, 7):
+        wire[wire_off[i] + 16 + int(rng.integers(0, 16))] ^= 0x10  # MAC failures
+    wire[wire_off[n - 3] + 2] ^= 0x20  # broken command name
+    wl[n - 5] = 20  # short frame (its bytes stay in place)
+    peer0 = np.full(S, 2, np.uint64)
+    verdict = _host_verdicts(wire, wire_off, wl, sid, [int(p) for p in peer0])
+    # the oracle applies the rules itself
+    opeer = peer0.copy()
+    out_off = in_off
+    out_bytes = int(out_off[-1]) + sizes[-1] + 16
+    rpl, rfl, rst = O.decode_batch(sess, opeer, sid, wire_off, wl, wire, out_off, out_bytes)
+    dec = C.CurveContext(0, S)
+    for s in range(S):
+        dec.session_set(s, precoms[s], O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    out = torch.zeros(out_bytes, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    dec.decode_batch(dev(torch, sid), dev(torch, wire_off), dev(torch, wl), dev(torch, wire), dev(torch, out_off),
+                     out, fl, st, verify_first=True, verdict_in=dev(torch, verdict))
+    torch.cuda.synchronize()
+    gst = host(st, np.int32)
+    assert np.array_equal(gst, rst), np.nonzero(gst != rst)[0][:10]
+    assert np.array_equal(host(fl, np.uint8), rfl)
+    assert (rst == 0x10000002).sum() > 10 and (rst == 0x11000001).sum() > 10
+    got = host(out, np.uint8)
+    for i in range(n):  # verified payloads, zeros for every failed frame's region
+        if wl[i] > 33:
+            a, b = int(out_off[i]), int(out_off[i]) + int(wl[i]) - 33
+            assert np.array_equal(got[a:b], rpl[a:b]), (i, sizes[i], int(rst[i]))
+    assert [dec.get_peer_nonce(s) for s in range(S)] == [2] * S  # the host keeps them

@@ -85,7 +85,7 @@ def run_pubsub(pub_kind, sub_kind, seed=5, heartbeat_ms=5, pub_zmtp30=False):
     """PUB (CURVE server) as pub_kind, SUB (CURVE client) as sub_kind: the
     SUB's SUBSCRIBE / CANCEL commands cross the two codecs; returns the SUB's
     counts (received, alpha, beta, gamma).  pub_zmtp30: the PUB announces
-    ZMTP 3.0 (tests/host/libzmq_zmtp30_test.patch), so the SUB takes
+    ZMTP 3.0 (tests/host/libzmq_test_switches.patch), so the SUB takes
     handshake_v3_0 (src/zmtp_engine.cpp:383-393) and its CURVE mechanism
     encodes subscriptions with downgrade_sub (src/curve_mechanism_base.cpp:
     118-158); the SUB's stderr then carries the patch's trace line, which
