@@ -30,12 +30,19 @@ JSON line fields beyond the driver contract:
                 profiles/ if a PMC summary for this workload was committed;
                 valu = the same kernel against the VALU issue peak (the bound
                 that binds: PMC instruction count / live launch duration).
-  cpu_baseline  the oracle's C restatement of curve_encoding_t with
-                libsodium's crypto_box_easy_afternm/open (dlopen) on host
-                threads, rank 0 at N=1 only, on a bounded sample.
   host_paths    the same round trip starting and ending in host memory
-                (PCIe-inclusive): zero-copy on pinned memory, and staged
-                through zmqg_*_host from pageable buffers.
+                (PCIe-inclusive): zero-copy on pinned memory, pinned
+                hipMemcpyAsync (with the GPU's PCIe link and NUMA placement),
+                staged through zmqg_*_host from pageable buffers; and the
+                deployable paths: the engine-hook bench and the libzmq CURVE
+                PUSH/PULL pairs, stock against the batched GPU codec.
+  hbm_fed       config 2 with every kernel input read from HBM (K batches with
+                their own buffers, beyond the 256 MiB Infinity Cache), with
+                its own decode roofline.
+  cpu_baseline  kind "reference": the stock libzmq build's curve_encoding_t
+                on the host cores, rank 0 at N=1 only, on a bounded sample;
+                beside it ("port") the oracle's C restatement of the framing
+                with libsodium's crypto_box_easy_afternm/open (dlopen).
 """
 import argparse
 import json
@@ -64,6 +71,11 @@ def parse():
                         "has passed (the clock ramp under sustained load; 0: none)")
     p.add_argument("--cold-pass", action="store_true",
                    help="also time each frame kernel on inputs from HBM (roofline.cold_launch_pass)")
+    p.add_argument("--hbm-sets", type=int, default=8,
+                   help="config-2 batches of the HBM-fed form (hbm_fed): each its own payload, wire and result "
+                        "buffers, so no kernel reads what the Infinity Cache still holds (0: skip)")
+    p.add_argument("--no-deployable", action="store_true",
+                   help="skip host_paths' deployable paths (the engine-hook bench and the libzmq CURVE pairs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-staged", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of CPU baseline sampling")
@@ -296,6 +308,11 @@ def main():
                 "note": f"{args.steps} encodes into {args.steps} wire buffers, then their {args.steps} decodes, each "
                         "run back to back between one event pair: inputs from HBM, not the MALL (launch_pass)"}
 
+    hbm = None
+    if args.hbm_sets > 0:
+        hbm = hbm_fed(torch, dev, stream, enc, dec, args.hbm_sets, n, W, P, sid, flags, in_off, lens, out_off, wlen,
+                      payload)
+
     total_msgs = n * args.steps * world
     gib = total_msgs * P / 2**30
     value = gib / elapsed
@@ -396,6 +413,7 @@ def main():
                    "frames_per_gpu": n, "payload_bytes": P, "wire_bytes": W, "sessions": 1,
                    "parallelism": f"frame-sharded x{world}, no collective"},
         "roofline": roofline,
+        "hbm_fed": hbm,
         "build": {"source_id": src_id, "commit": commit},
     }
 
@@ -406,9 +424,17 @@ def main():
     if rank == 0 and world == 1 and not args.no_host_staged:
         result["host_paths"] = host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_off, lens,
                                           out_off, wlen, n, P, W)
+    if rank == 0 and world == 1 and not args.no_deployable:
+        result.setdefault("host_paths", {}).update(deployable_paths())
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(payload.cpu().numpy(), precom, n, P, W, flags_np, args.cpu_seconds)
+        port = cpu_baseline(payload.cpu().numpy(), precom, n, P, W, flags_np, args.cpu_seconds)
+        ref = cpu_baseline_reference(P, args.cpu_seconds)
+        if ref is not None:
+            ref["port"] = port
+            result["cpu_baseline"] = ref
+        else:
+            result["cpu_baseline"] = port
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -487,6 +513,59 @@ def launch_pass(torch, dev, stream, enc, dec, K, n, W, P, sid, flags, in_off, le
     assert all(int((st != 0).sum()) == 0 for st in sts), "launch pass: decode failures"
     assert torch.equal(back, payload), "launch pass: round trip mismatch"
     return ev[0].elapsed_time(ev[1]) / K / 1e3, ev[2].elapsed_time(ev[3]) / K / 1e3
+
+
+def hbm_fed(torch, dev, stream, enc, dec, K, n, W, P, sid, flags, in_off, lens, out_off, wlen, payload):
+    """Config 2 with every input fed from HBM (verdict r5 item 2): K batches,
+    each with its own payload, wire and result buffers (K x ~200 MB, against
+    the 256 MiB Infinity Cache), encoded back to back between one event pair
+    (each reads a payload last touched K batches ago), then decoded back to
+    back between another (each reads a wire written K encodes ago).  Rate =
+    the K round trips' payload over the two spans; per-launch durations =
+    span / K, with the decode frame kernel's roofline as in the main line.
+    Every decode's statuses and payload are checked."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xFEED)
+    pays = [payload] + [torch.randint(0, 256, (n * P,), dtype=torch.uint8, device=dev, generator=g)
+                        for _ in range(K - 1)]
+    wires = [torch.empty(n * W, dtype=torch.uint8, device=dev) for _ in range(K)]
+    backs = [torch.empty(n * P, dtype=torch.uint8, device=dev) for _ in range(K)]
+    fls = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(K)]
+    sts = [torch.full((n,), -1, dtype=torch.int32, device=dev) for _ in range(K)]
+
+    def run():
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record(stream)
+        for k in range(K):
+            enc.encode_batch(sid, None, flags, in_off, lens, pays[k], out_off, wires[k], stream, max_len=P,
+                             nonce_auto=True)
+        ev[1].record(stream)
+        ev[2].record(stream)
+        for k in range(K):
+            dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream, max_len=W)
+        ev[3].record(stream)
+        torch.cuda.synchronize(dev)
+        return ev[0].elapsed_time(ev[1]) / 1e3, ev[2].elapsed_time(ev[3]) / 1e3
+
+    run()  # first touch of the new buffers; the clock stays up from the main line
+    es, ds = run()
+    for k in range(K):
+        assert int((sts[k] != 0).sum()) == 0 and torch.equal(backs[k], pays[k]), "hbm_fed: round trip mismatch"
+    e, d = es / K, ds / K
+    dec_read = n * (P + 49)
+    achieved = dec_read / d / 1e9
+    out = {"value": K * n * P / 2**30 / (es + ds), "unit": "GiB/s", "msgs_per_s": K * n / (es + ds),
+           "ms_per_step": 1e3 * (es + ds) / K, "encode_us": e * 1e6, "decode_us": d * 1e6,
+           "roofline": {"bound": "hbm", "kernel": ROOF_KERNEL, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "algorithmic_bytes_per_launch": dec_read,
+                        "avg_launch_us": d * 1e6},
+           "sets": K, "bytes_per_set": n * (2 * P + W),
+           "note": f"{K} config-2 batches with their own buffers ({K * n * (2 * P + W) / 2**20:.0f} MiB against "
+                   f"the 256 MiB Infinity Cache): {K} encodes back to back, then their {K} decodes, one event pair "
+                   "each; every input comes from HBM"}
+    del pays, wires, backs
+    torch.cuda.empty_cache()
+    return out
 
 
 def device_census(torch, world, local):
@@ -669,7 +748,27 @@ def host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_o
     out["zerocopy_pinned"] = {"value": 4 * n * P / 2**30 / (t1 - t0), "unit": "GiB/s",
                               "note": "encode+decode, kernels on pinned host memory over PCIe"}
 
+    place = gpu_placement(torch, local)
+    place["payload_buffer_node"] = page_node(hp.data_ptr())
     out["pinned_dma"] = pinned_dma(C, torch, dev, local, hp, precom, flags, flags_np, n, P, W)
+    out["pinned_dma"]["placement"] = place
+    # the same with the pinned buffers allocated (and this thread running) on
+    # the GPU's own NUMA node, when that is not where they were
+    try:
+        gnode = int(place.get("numa_node") or -1)
+    except ValueError:
+        gnode = -1
+    cpus = node_cpus(gnode) if gnode >= 0 else set()
+    if cpus and place["payload_buffer_node"] not in (None, gnode):
+        keep = os.sched_getaffinity(0)
+        try:
+            os.sched_setaffinity(0, cpus)
+            hpl = payload.cpu().pin_memory()
+            local_dma = pinned_dma(C, torch, dev, local, hpl, precom, flags, flags_np, n, P, W)
+            local_dma["payload_buffer_node"] = page_node(hpl.data_ptr())
+            out["pinned_dma_gpu_node"] = local_dma
+        finally:
+            os.sched_setaffinity(0, keep)
 
     hpn = hp.numpy()
     hin = np.arange(n, dtype=np.uint64) * P
@@ -692,6 +791,61 @@ def host_paths(C, torch, dev, local, payload, precom, flags, flags_np, sid, in_o
     out["pageable_staged"] = {"value": reps * n * P / 2**30 / (t1 - t0), "unit": "GiB/s",
                               "note": "zmqg_encode_host + zmqg_decode_host, pageable buffers, H2D+D2H included"}
     return out
+
+
+def page_node(addr):
+    """NUMA node holding the page at host address `addr` (get_mempolicy with
+    MPOL_F_NODE | MPOL_F_ADDR), or None."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        mode = ctypes.c_int(-1)
+        rc = libc.syscall(239, ctypes.byref(mode), None, ctypes.c_ulong(0), ctypes.c_void_p(addr), ctypes.c_ulong(3))
+        return mode.value if rc == 0 else None
+    except Exception:
+        return None
+
+
+def gpu_placement(torch, local):
+    """The GPU's PCIe link and NUMA node (sysfs), and the NUMA nodes of the
+    CPUs this process may run on (verdict r5 item 7: the pinned-DMA rate's
+    spread from box to box)."""
+    def rd(path):
+        try:
+            return open(path).read().strip()
+        except OSError:
+            return None
+    p = torch.cuda.get_device_properties(local)
+    addr = None
+    dom, bus, devn = (getattr(p, f, None) for f in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if bus is not None:
+        addr = f"{dom or 0:04x}:{bus:02x}:{devn:02x}.0"
+    out = {"pci": addr}
+    if addr:
+        base = f"/sys/bus/pci/devices/{addr}"
+        for k in ("numa_node", "current_link_width", "current_link_speed", "max_link_width", "max_link_speed"):
+            out[k] = rd(f"{base}/{k}")
+    nodes = set()
+    for c in os.sched_getaffinity(0):
+        try:
+            nodes.update(int(x[4:]) for x in os.listdir(f"/sys/devices/system/cpu/cpu{c}") if x.startswith("node"))
+        except OSError:
+            pass
+    out["process_cpu_nodes"] = sorted(nodes)
+    return out
+
+
+def node_cpus(node):
+    """The CPUs of NUMA node `node` this process may use."""
+    try:
+        txt = open(f"/sys/devices/system/node/node{node}/cpulist").read().strip()
+    except OSError:
+        return set()
+    cpus = set()
+    for part in txt.split(","):
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus & os.sched_getaffinity(0)
 
 
 def pinned_dma(C, torch, dev, local, hp, precom, flags, flags_np, n, P, W, chunks=8, reps=4):
@@ -783,6 +937,81 @@ def pinned_dma(C, torch, dev, local, hp, precom, flags, flags_np, n, P, W, chunk
             "note": f"encode+decode round trip, pinned host buffers, hipMemcpyAsync H2D/D2H, send and receive "
                     f"pipelines on their own copy and compute streams, {chunks} slices (P + W bytes each way per "
                     f"message)"}
+
+
+def deployable_paths():
+    """What a libzmq user gets from the batched codec (verdict r5 item 4):
+      engine_hook    tests/host/test_engine_hook.cpp bench -- two epoll I/O
+                     threads, client engines encoding on the GPU, socketpairs,
+                     server engines decoding on the GPU (curve_io_hook_t /
+                     curve_engine_link_t), messages/s;
+      libzmq_pairs   CURVE PUSH/PULL over tcp://127.0.0.1 between two builds
+                     of the reference libzmq (tests/host/build_libzmq.sh):
+                     stock (libsodium) and zmqgb (the batched GPU codec inside
+                     the stream engine), 1,000,000 messages of config 1's plan
+                     per run, receiver's msg/s, runs interleaved
+                     (tools/libzmq_pair_bench.py)."""
+    import subprocess
+    out = {}
+    exe = os.path.join(ROOT, "tests", "host", "bin", "engine_hook_bench")
+    if os.path.exists(exe):
+        runs = {}
+        for conns, msgs, size in ((16, 20000, 1024), (64, 20000, 256)):
+            r = subprocess.run(["timeout", "-k", "10", "120", exe, "bench", str(conns), str(msgs), str(size)],
+                               capture_output=True, text=True)
+            f = r.stdout.split()
+            if r.returncode == 0 and f and f[0] == "RATE":
+                runs[f"{conns}x{msgs}x{size}B"] = {"msgs_per_s": float(f[f.index("msgs_per_s") + 1]),
+                                                    "payload_MB_per_s": float(f[f.index("payload_MB_per_s") + 1])}
+            else:
+                runs[f"{conns}x{msgs}x{size}B"] = {"error": (r.stderr or r.stdout)[-300:]}
+        out["engine_hook"] = {"runs": runs, "unit": "msgs/s",
+                              "note": "tests/host/test_engine_hook.cpp bench: two epoll I/O threads, GPU encode "
+                                      "and decode through curve_io_hook_t, non-blocking socketpairs"}
+    else:
+        out["engine_hook"] = None
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import libzmq_pair_bench as lpb
+        if os.path.exists(os.path.join(lpb.BIN, "interop_zmqgb")):
+            r = lpb.run((("stock", "stock"), ("zmqgb", "zmqgb")), reps=3, n=1000000)
+            out["libzmq_pairs"] = {k: {"msgs_per_s": v["msgs_per_s"], "median_msgs_per_s": v["median_msgs_per_s"]}
+                                   for k, v in r.items()}
+            out["libzmq_pairs"]["note"] = ("CURVE PUSH/PULL over tcp://127.0.0.1, 1,000,000 messages (1 KiB plus "
+                                           "config 1's 0 B - 64 KiB and multipart ones), every byte checked, "
+                                           "heartbeats every 5 ms; stock = reference libzmq + libsodium, zmqgb = "
+                                           "the same sources with the batched GPU codec in the stream engine")
+        else:
+            out["libzmq_pairs"] = None
+    except Exception as e:  # a failed pairing is reported, not fatal to the line
+        out["libzmq_pairs"] = {"error": str(e)[-300:]}
+    return out
+
+
+def cpu_baseline_reference(P, seconds):
+    """cpu_baseline of kind "reference": the stock libzmq build's own
+    zmq::curve_encoding_t (src/curve_mechanism_base.cpp compiled where it lies,
+    libsodium 1.0.18), driven as unittests/unittest_curve_encoding.cpp:26-71
+    drives it -- tests/host/curve_encoding_ref_bench.cpp, one client/server
+    pair per thread, every decoded payload checked.  None when the program was
+    not built (no reference at build time)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "host", "_ref", "libzmq", "curve_encoding_ref_bench")
+    if not os.path.exists(exe):
+        return None
+    threads, affinity, quota = host_cores()
+    r = subprocess.run(["timeout", "-k", "10", str(int(seconds) + 60), exe, str(threads), str(P), str(seconds)],
+                       capture_output=True, text=True)
+    f = r.stdout.split()
+    if r.returncode != 0 or not f or f[0] != "RATE":
+        return None
+    msgs_s = float(f[f.index("msgs_per_s") + 1])
+    return {"value": float(f[f.index("payload_GiB_per_s") + 1]), "unit": "GiB/s", "cores": threads,
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(), "kind": "reference",
+            "msgs_per_s": msgs_s,
+            "sample": f"{int(f[f.index('msgs') + 1])} encode+decode round trips of {P} B over "
+                      f"{float(f[f.index('seconds') + 1]):.2f} s on {threads} threads: the stock build's "
+                      "zmq::curve_encoding_t (tests/host/curve_encoding_ref_bench.cpp)"}
 
 
 def host_cores():

@@ -3,6 +3,7 @@
 
 #include <errno.h>
 #include <string.h>
+#include <time.h>
 
 namespace zmqg
 {
@@ -17,6 +18,13 @@ size_t align256 (size_t x)
 //  flags byte + up to 10 bytes of a downgraded SUBSCRIBE/CANCEL prefix
 //  (src/curve_mechanism_base.cpp:113-128, 169)
 const size_t max_wire_growth = 8 + 8 + 16 + 1 + 10;
+
+uint64_t mono_ns ()
+{
+    timespec t;
+    clock_gettime (CLOCK_MONOTONIC, &t);
+    return static_cast<uint64_t> (t.tv_sec) * 1000000000u + t.tv_nsec;
+}
 }
 
 curve_batcher_t::curve_batcher_t (zmqg_ctx *ctx_,
@@ -30,6 +38,7 @@ curve_batcher_t::curve_batcher_t (zmqg_ctx *ctx_,
     _out_cap (0)
 {
     _open[0] = _open[1] = NULL;
+    _stats.batch_ns = _stats.fence_ns = _stats.launches = 0;
 }
 
 curve_batcher_t::~curve_batcher_t ()
@@ -238,6 +247,7 @@ int curve_batcher_t::submit_decode (curve_encoding_gpu_t *conn_,
 int curve_batcher_t::launch (slot_t *s)
 {
     int rc;
+    const uint64_t t0 = mono_ns ();
     //  the slot's longest frame bounds the batch: a slot of small messages
     //  (every stream within the frame kernel's 4.5 KiB) skips the
     //  large-frame launches
@@ -263,6 +273,7 @@ int curve_batcher_t::launch (slot_t *s)
                                    s->in, s->out_off, s->in, s->flags_out,
                                    s->status, &o, _stream);
     }
+    const uint64_t t1 = mono_ns ();
     if (rc == 0)
         rc = _config.notify_fd >= 0
                ? zmqg_fence_record_notify (_ctx, _stream, _config.notify_fd,
@@ -275,6 +286,9 @@ int curve_batcher_t::launch (slot_t *s)
         return -1;
     }
     _flight.push_back (s);
+    _stats.batch_ns += t1 - t0;
+    _stats.fence_ns += mono_ns () - t1;
+    ++_stats.launches;
     return 0;
 }
 

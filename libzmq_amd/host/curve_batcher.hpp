@@ -143,6 +143,14 @@ class curve_batcher_t
     //  slots launched and not yet delivered
     size_t batches_in_flight () const { return _flight.size (); }
 
+    //  host time spent in the device calls of launch (): the batch call and
+    //  the fence (+ notification), nanoseconds since construction
+    struct launch_stats_t
+    {
+        uint64_t batch_ns, fence_ns, launches;
+    };
+    const launch_stats_t &launch_stats () const { return _stats; }
+
   private:
     enum kind_t
     {
@@ -185,6 +193,7 @@ class curve_batcher_t
     std::vector<slot_t *> _free;
     slot_t *_open[2];
     std::deque<slot_t *> _flight;
+    launch_stats_t _stats;
 
     curve_batcher_t (const curve_batcher_t &);
     curve_batcher_t &operator= (const curve_batcher_t &);

@@ -2,11 +2,42 @@
 #include "curve_engine_hook.hpp"
 
 #include <errno.h>
+#include <string.h>
 #include <sys/eventfd.h>
 #include <unistd.h>
 
 namespace zmqg
 {
+void result_fifo_t::push (const uint8_t *data_, size_t size_, uint8_t flags_)
+{
+    if (_tail + size_ > _buf.size ()) {
+        if (_head > 0) {
+            //  (the records before _head are gone: slide the rest down)
+            memmove (&_buf[0], &_buf[0] + _head, _tail - _head);
+            _tail -= _head;
+            _head = 0;
+        }
+        if (_tail + size_ > _buf.size ()) {
+            size_t cap = _buf.size () ? _buf.size () * 2 : 64u << 10;
+            while (cap < _tail + size_)
+                cap *= 2;
+            _buf.resize (cap);
+        }
+    }
+    if (size_)
+        memcpy (&_buf[0] + _tail, data_, size_);
+    _tail += size_;
+    _recs.push_back (std::make_pair (size_, flags_));
+}
+
+void result_fifo_t::pop ()
+{
+    _head += _recs.front ().first;
+    _recs.pop_front ();
+    if (_recs.empty ())
+        _head = _tail = 0;
+}
+
 namespace
 {
 //  the hook's wake-up descriptor, as the mailbox's signaler makes its own
@@ -136,7 +167,7 @@ void curve_io_hook_t::on_encoded (uint64_t tag_,
         return; //  closed while in flight
     --l->_send_pending;
     const bool first = l->_encoded.empty ();
-    l->_encoded.push_back (std::vector<uint8_t> (wire_, wire_ + size_));
+    l->_encoded.push (wire_, size_, 0);
     if (first)
         _out_ready.push_back (tag_);
 }
@@ -163,10 +194,7 @@ void curve_io_hook_t::on_decoded (uint64_t tag_,
         _in_ready.push_back (tag_);
         return;
     }
-    msg_buf_t m;
-    m.bytes.assign (payload_, payload_ + size_);
-    m.flags = flags_;
-    l->_decoded.push_back (m);
+    l->_decoded.push (payload_, size_, flags_);
     if (first)
         _in_ready.push_back (tag_);
 }
@@ -213,8 +241,19 @@ bool curve_engine_link_t::next_encoded (std::vector<uint8_t> &wire_)
 {
     if (_encoded.empty ())
         return false;
-    wire_.swap (_encoded.front ());
-    _encoded.pop_front ();
+    wire_.assign (_encoded.front_data (),
+                  _encoded.front_data () + _encoded.front_size ());
+    _encoded.pop ();
+    return true;
+}
+
+bool curve_engine_link_t::peek_encoded (const uint8_t **wire_,
+                                        size_t *size_) const
+{
+    if (_encoded.empty ())
+        return false;
+    *wire_ = _encoded.front_data ();
+    *size_ = _encoded.front_size ();
     return true;
 }
 
@@ -236,9 +275,22 @@ bool curve_engine_link_t::next_decoded (msg_buf_t &msg_)
 {
     if (_decoded.empty ())
         return false;
-    msg_.bytes.swap (_decoded.front ().bytes);
-    msg_.flags = _decoded.front ().flags;
-    _decoded.pop_front ();
+    msg_.bytes.assign (_decoded.front_data (),
+                       _decoded.front_data () + _decoded.front_size ());
+    msg_.flags = _decoded.front_flags ();
+    _decoded.pop ();
+    return true;
+}
+
+bool curve_engine_link_t::peek_decoded (const uint8_t **payload_,
+                                        size_t *size_,
+                                        uint8_t *flags_) const
+{
+    if (_decoded.empty ())
+        return false;
+    *payload_ = _decoded.front_data ();
+    *size_ = _decoded.front_size ();
+    *flags_ = _decoded.front_flags ();
     return true;
 }
 }

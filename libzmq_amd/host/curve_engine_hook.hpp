@@ -70,6 +70,28 @@ namespace zmqg
 {
 class curve_engine_link_t;
 
+//  Results waiting for their engine: the bytes back to back in one growing
+//  buffer, (size, flags) per record -- no allocation per message once the
+//  buffer has grown to the connection's working depth.
+class result_fifo_t
+{
+  public:
+    result_fifo_t () : _head (0), _tail (0) {}
+    void push (const uint8_t *data_, size_t size_, uint8_t flags_);
+    bool empty () const { return _recs.empty (); }
+    size_t size () const { return _recs.size (); }
+    //  the oldest record; valid until the next push
+    const uint8_t *front_data () const { return &_buf[0] + _head; }
+    size_t front_size () const { return _recs.front ().first; }
+    uint8_t front_flags () const { return _recs.front ().second; }
+    void pop ();
+
+  private:
+    std::vector<uint8_t> _buf;
+    size_t _head, _tail;
+    std::deque<std::pair<size_t, uint8_t> > _recs;
+};
+
 //  The engine's resume points (implemented by the engine).  Called from the
 //  hook's in_event () / timer_event () / iteration () / drain (), never from
 //  inside a submit.
@@ -118,6 +140,10 @@ class curve_io_hook_t : private curve_sink_t
     //  launched batches whose results have not been delivered yet (a poller
     //  that holds new messages back while the device is busy uses it)
     size_t batches_in_flight () const { return _batcher.batches_in_flight (); }
+    const curve_batcher_t::launch_stats_t &launch_stats () const
+    {
+        return _batcher.launch_stats ();
+    }
 
   private:
     friend class curve_engine_link_t;
@@ -156,6 +182,10 @@ class curve_engine_link_t
     int submit_send (const uint8_t *data_, size_t size_, uint8_t msg_flags_);
     //  the next encoded MESSAGE command, in submission order
     bool next_encoded (std::vector<uint8_t> &wire_);
+    //  the same without a copy: the command's bytes stay valid until the
+    //  next pop_encoded or hook call
+    bool peek_encoded (const uint8_t **wire_, size_t *size_) const;
+    void pop_encoded () { _encoded.pop (); }
 
     //  in side: the body of one ZMTP MESSAGE frame.  0, or -1 with errno
     //  (EPIPE: the connection has already failed)
@@ -163,6 +193,11 @@ class curve_engine_link_t
     //  the next decoded message (payload, MORE/COMMAND flags), in receive
     //  order; after a failure only those decoded before it
     bool next_decoded (msg_buf_t &msg_);
+    //  the same without a copy (valid until pop_decoded or a hook call)
+    bool peek_decoded (const uint8_t **payload_,
+                       size_t *size_,
+                       uint8_t *flags_) const;
+    void pop_decoded () { _decoded.pop (); }
     //  0, or the first failure's ZMQ_PROTOCOL_ERROR_ZMTP_* code
     int failed () const { return _failed; }
 
@@ -178,8 +213,7 @@ class curve_engine_link_t
     curve_encoding_gpu_t *const _codec;
     curve_link_events_t *const _events;
     const uint64_t _id;
-    std::deque<std::vector<uint8_t> > _encoded;
-    std::deque<msg_buf_t> _decoded;
+    result_fifo_t _encoded, _decoded;
     size_t _send_pending, _recv_pending;
     int _failed;
 

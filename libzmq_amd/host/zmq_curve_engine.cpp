@@ -47,6 +47,16 @@ size_t max_bytes ()
     static const size_t v = env_size ("ZMQG_ENGINE_BYTES", 16u << 20);
     return v;
 }
+//  the send side pulls from the session only when fewer messages than this
+//  are still to be written (in the batch, on the device or encoded): pulling
+//  on every out_event would empty the pipe each time, and the sender's next
+//  message would then wake this thread through the mailbox (the pipe's
+//  activate_read) for a handful of messages
+size_t low_water ()
+{
+    static const size_t v = env_size ("ZMQG_ENGINE_LOW_WATER", 512);
+    return v;
+}
 
 uint64_t now_ms ()
 {
@@ -104,11 +114,15 @@ class curve_io_poll_t : public i_poll_events
             fprintf (stderr,
                      "zmqg engine: %llu wake-ups, %llu launches, %llu "
                      "messages launched, %llu delivered by wake-ups, "
-                     "%.3f ms in launches, %.3f ms in deliveries\n",
+                     "%.3f ms in launches (%llu batch calls %.3f ms, "
+                     "fences %.3f ms), %.3f ms in deliveries\n",
                      (unsigned long long) _wakes,
                      (unsigned long long) _launches,
                      (unsigned long long) _launched,
                      (unsigned long long) _delivered, _launch_ns * 1e-6,
+                     (unsigned long long) _hook->launch_stats ().launches,
+                     _hook->launch_stats ().batch_ns * 1e-6,
+                     _hook->launch_stats ().fence_ns * 1e-6,
                      _deliver_ns * 1e-6);
         delete _hook;
     }
@@ -126,6 +140,7 @@ class curve_io_poll_t : public i_poll_events
         _users (0),
         _timer (false),
         _max_flight (env_size ("ZMQG_ENGINE_FLIGHT", 2)),
+        _min_batch (env_size ("ZMQG_ENGINE_MIN_BATCH", 64)),
         _wakes (0),
         _launches (0),
         _launched (0),
@@ -153,8 +168,12 @@ class curve_io_poll_t : public i_poll_events
     //  completion (in_event), so a loaded thread launches big batches.
     void launch_if_idle ()
     {
-        if (!_hook->flush_pending ()
-            || _hook->batches_in_flight () >= _max_flight)
+        const size_t flying = _hook->batches_in_flight ();
+        //  an idle device takes any batch (latency); a busy one only a
+        //  batch worth a launch, else the completion's wake-up sends it
+        if (!_hook->flush_pending () || flying >= _max_flight
+            || (flying > 0
+                && _hook->outstanding () - _hook->in_flight () < _min_batch))
             return;
         ++_launches;
         _launched += _hook->outstanding () - _hook->in_flight ();
@@ -171,6 +190,7 @@ class curve_io_poll_t : public i_poll_events
     int _users;
     bool _timer;
     const size_t _max_flight;
+    const size_t _min_batch;
     //  ZMQG_ENGINE_STATS: printed when the thread exits
     uint64_t _wakes, _launches, _launched, _delivered, _launch_ns, _deliver_ns;
     const bool _stats;
@@ -322,7 +342,9 @@ void curve_engine_codec_t::pull_into_batch ()
 
 int curve_engine_codec_t::take_encoded (msg_t *msg_)
 {
-    if (!_link.next_encoded (_wire)) {
+    const uint8_t *wire;
+    size_t size;
+    if (!_link.peek_encoded (&wire, &size)) {
         errno = EAGAIN;
         return -1;
     }
@@ -330,15 +352,17 @@ int curve_engine_codec_t::take_encoded (msg_t *msg_)
     _tx_sizes.pop_front ();
     //  the MESSAGE command is a fresh msg_t without flags, as msg_->move
     //  (msg_box) leaves it (src/curve_mechanism_base.cpp:203)
-    const int rc = msg_->init_size (_wire.size ());
+    const int rc = msg_->init_size (size);
     errno_assert (rc == 0);
-    memcpy (msg_->data (), &_wire[0], _wire.size ());
+    memcpy (msg_->data (), wire, size);
+    _link.pop_encoded ();
     return 0;
 }
 
 int curve_engine_codec_t::pull_and_encode (msg_t *msg_)
 {
-    pull_into_batch ();
+    if (_link.sends_in_flight () + _link.encoded_queued () < low_water ())
+        pull_into_batch ();
     if (take_encoded (msg_) == 0)
         return 0;
     if (_tx_error) {
@@ -524,16 +548,20 @@ int curve_engine_codec_t::deliver ()
     int rc = 1;
     for (;;) {
         if (!_rx_held) {
-            if (!_link.next_decoded (_rx))
+            const uint8_t *payload;
+            size_t size;
+            uint8_t flags;
+            if (!_link.peek_decoded (&payload, &size, &flags))
                 break;
             _rx_bytes -= _rx_sizes.front ();
             _rx_sizes.pop_front ();
-            int r = _rx_msg.init_size (_rx.size ());
+            int r = _rx_msg.init_size (size);
             errno_assert (r == 0);
-            if (_rx.size ())
-                memcpy (_rx_msg.data (), _rx.data (), _rx.size ());
+            if (size)
+                memcpy (_rx_msg.data (), payload, size);
+            _link.pop_decoded ();
             //  the plaintext MORE / COMMAND bits, ORed as set_flags does
-            _rx_msg.set_flags (_rx.flags);
+            _rx_msg.set_flags (flags);
             //  the reference's per-message work before the push (:625-640)
             if (e->_has_timeout_timer) {
                 e->_has_timeout_timer = false;

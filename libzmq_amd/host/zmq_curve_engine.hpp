@@ -134,12 +134,10 @@ class curve_engine_codec_t : public zmqg::curve_link_events_t
 
     msg_t _pulled;   //  a session message too large for a slot, held
     bool _big_held;  //  until the connection has nothing in flight
-    std::vector<uint8_t> _wire;
     std::deque<size_t> _tx_sizes; //  payload bytes of the sends pending
     size_t _tx_bytes;
     bool _tx_error; //  the device refused a submission: sending stops
 
-    zmqg::msg_buf_t _rx;
     msg_t _rx_msg;  //  a decoded message the session's pipe refused
     bool _rx_held;
     size_t _rx_bytes; //  wire bytes submitted and not yet delivered

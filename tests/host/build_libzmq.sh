@@ -109,6 +109,12 @@ link () {
 
 variant stock "" libzmq_test_switches.patch
 link stock
+# the CPU baseline on the stock build's own curve_encoding_t (bench.py)
+# (libsodium through a directory of its own: an rpath to $SODIUM/lib would
+# also pick that tree's older libstdc++ for the program)
+mkdir -p "$OUT/sodium" && ln -sf "$SODIUM/lib/libsodium.so.23" "$OUT/sodium/libsodium.so.23"
+g++ $CXXFLAGS $inc -o "$OUT/curve_encoding_ref_bench" "$HERE/curve_encoding_ref_bench.cpp" \
+  "$OUT/stock/libzmq.so.5" "$OUT/sodium/libsodium.so.23" -Wl,-rpath,'$ORIGIN/stock:$ORIGIN/sodium' -lpthread
 
 variant zmqg "-DZMQ_USE_ZMQG_CURVE" libzmq_test_switches.patch libzmq_zmqg.patch
 link zmqg curve_encoding_gpu.cpp

@@ -5,7 +5,7 @@
 # writes <out prefix>.pull.err / .push.err (prof / cpu / zmqg engine lines).
 set -e
 B=$(cd "$(dirname "$0")/.." && pwd)/tests/host/_ref/libzmq
-S=$1; C=$2; O=$3; N=${4:-100000}
+S=$1; C=$2; O=$3; N=${4:-1000000}
 P=$(python3 -c 'import socket;s=socket.socket();s.bind(("127.0.0.1",0));print(s.getsockname()[1])')
 Q=$((P + 1))
 export INTEROP_THREAD_CPU=1 ZMQG_ENGINE_STATS=1
