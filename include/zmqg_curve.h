@@ -359,9 +359,14 @@ int zmqg_fence_wait(zmqg_ctx *ctx, uint64_t fence);
  * counter semantics; a pipe's write end works too) from a HIP runtime thread,
  * and from then on zmqg_fence_query of that fence returns 1.  The poller
  * watches `fd` for POLLIN, reads it, and polls its fences.  `fd` must stay
- * open until zmqg_notify_quiesce has returned: that call waits until every
+ * open until zmqg_notify_quiesce has returned 0: that call waits until every
  * notification enqueued on the ctx so far has been delivered (the streams
- * must be able to reach them).  zmqg_ctx_destroy waits for them too.
+ * must be able to reach them), at most ~10 s: -ETIMEDOUT then (a stuck
+ * stream), and `fd` must stay open.  zmqg_ctx_destroy waits for them too and,
+ * on such a timeout, returns -ETIMEDOUT with the ctx's host state left
+ * allocated for the late host functions.  If the fence is recorded but its
+ * notification cannot be queued, the call fails with *fence_out set (the
+ * fence can still be waited for); a failure before the fence leaves it 0.
  * (Replaces no reference symbol: the reference codec is synchronous.) */
 int zmqg_fence_record_notify(zmqg_ctx *ctx, void *stream, int fd, uint64_t *fence_out);
 int zmqg_notify_quiesce(zmqg_ctx *ctx);

@@ -57,6 +57,9 @@ __device__ __forceinline__ void seq_store4(uint64_t a, uint32_t x, uint32_t y, u
         *(G4_ *) (uintptr_t) a = (v4_){x, y, z, w};
 }
 
+#ifndef ZMQG_SEQ_PF
+#define ZMQG_SEQ_PF 1 // k_frames_seq: windows requested ahead of the one computed (1; 2 measured slower)
+#endif
 #ifndef ZMQG_SEQ_AL64
 #define ZMQG_SEQ_AL64 1 // k_frames_seq decode: 64-byte payload chunks when every payload of a wave starts 64-byte aligned (0: off, for timing)
 #endif
@@ -1337,9 +1340,18 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     const uint32_t lim = S + v; // stream words whose first byte is below lim hold a stream byte
     const uint64_t wave_end = wave_max_u64(nw ? A + S : 0); // end of the wave's furthest frame: reads below it stay in the buffer
     // window 1's words (word 0 is window 0's word 16, d0); windows t and t+1
-    // alternate between the two buffers
+    // alternate between the two buffers -- or, ZMQG_SEQ_PF 2, windows 1 and
+    // 2 are requested here and windows rotate over three buffers, each
+    // requested two steps before it is used (inputs from HBM rather than the
+    // Infinity Cache take longer than one keystream to arrive)
     uint32_t ddA[16], ddB[16];
     bool fastA = nw > 1u ? frame_prefetch(A4, lim, wave_end, 1u, ddA) : true, fastB = true;
+#if ZMQG_SEQ_PF == 2
+    uint32_t ddC[16];
+    bool fastC = true;
+    if (nw > 2u)
+        fastB = frame_prefetch(A4, lim, wave_end, 2u, ddB);
+#endif
 
     // Decode output in 64-byte payload chunks when every lane's payload
     // starts on a 64-byte boundary (wave-uniform; e.g. packed 1 KiB
@@ -1454,6 +1466,11 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     auto step = [&](uint32_t t, uint32_t (&dd)[16], bool &fast, uint32_t (&dn)[16], bool &fastn) {
         SEQ_STAMP(3u + t);
         const bool act = t < nw;
+#if ZMQG_SEQ_PF == 2
+        // window t+2 into the buffer window t-1 has left
+        if (t + 2u < nw)
+            fastn = frame_prefetch(A4, lim, wave_end, t + 2u, dn);
+#endif
         uint32_t ks[16];
         if (ZMQG_FRAMES_ABLATE & 32) {
 #pragma unroll
@@ -1546,7 +1563,7 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
             for (int k = 0; k < 16; ++k)
                 dn[k] = y[k] + k;
             fastn = true;
-        } else if (t + 1u < nw) {
+        } else if (ZMQG_SEQ_PF == 1 && t + 1u < nw) {
             fastn = frame_prefetch(A4, lim, wave_end, t + 1u, dn);
         }
         if (t < 8u)
@@ -1610,6 +1627,20 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     // as the compiler's wait analysis knows, and every step would then wait
     // for all loads before its first write of a buffer register)
     if (steps > 1u) {
+#if ZMQG_SEQ_PF == 2
+#pragma unroll 1
+        for (uint32_t t = 1;; t += 3) {
+            step(t, ddA, fastA, ddC, fastC);
+            if (t + 1u >= steps)
+                break;
+            step(t + 1u, ddB, fastB, ddA, fastA);
+            if (t + 2u >= steps)
+                break;
+            step(t + 2u, ddC, fastC, ddB, fastB);
+            if (t + 3u >= steps)
+                break;
+        }
+#else
 #pragma unroll 1
         for (uint32_t t = 1;; t += 2) {
             step(t, ddA, fastA, ddB, fastB);
@@ -1619,6 +1650,7 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
             if (t + 2u >= steps)
                 break;
         }
+#endif
     }
     SEQ_STAMP(60u);
     // the last window's MAC

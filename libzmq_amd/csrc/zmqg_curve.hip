@@ -261,10 +261,15 @@ struct zmqg_ctx {
     } while (0)
 
 // The ctx's work is ordered by stream: a batch call runs on the caller's
-// stream (which then becomes the ctx's last stream); a call that switches
-// to another stream first makes it wait for everything queued on the last
-// one (an event recorded there).  The null stream is a stream like any
-// other: with own_stream non-blocking it is not ordered implicitly.
+// stream (which then becomes the ctx's last stream); every call that uses
+// the ctx's workspace or sessions on another stream than the last one --
+// the batch calls, the session installs and accessors, the per-message
+// calls -- first makes it wait for everything queued on the last one (an
+// event recorded there, order_after_last; nothing when the stream is the
+// same).  The null stream is a stream like any other: with own_stream
+// non-blocking it is not ordered implicitly.
+static int notify_wait(zmqg_ctx *ctx);
+
 static void set_last(zmqg_ctx *ctx, hipStream_t st)
 {
     ctx->last_stream = st;
@@ -2486,9 +2491,9 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
         (void) hipHostFree(ctx->sinst);
     if (ctx->order_ev)
         (void) hipEventDestroy(ctx->order_ev);
-    // notification host functions still queued hold the ctx
-    while (ctx->notify_pending.load(std::memory_order_acquire) > 0)
-        sched_yield();
+    // notification host functions still queued hold the ctx: after ~10 s
+    // without them the ctx is left allocated (leaked, not freed under them)
+    const int quiet = notify_wait(ctx);
     if (ctx->own_stream)
         (void) hipStreamDestroy(ctx->own_stream);
     for (auto &v : ctx->prof)
@@ -2502,6 +2507,8 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
         (void) hipEventDestroy(f.second);
     for (hipEvent_t e : ctx->fence_pool)
         (void) hipEventDestroy(e);
+    if (quiet != 0)
+        return quiet;
     delete ctx;
     return 0;
 }
@@ -2798,8 +2805,12 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
         return -EINVAL;
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    set_last(ctx, st);
-    int rc = ensure_workspace(ctx, n, st);
+    // the workspace and the call state are shared with the ctx's other
+    // streams: this call runs after the work queued on the last one
+    int rc = order_after_last(ctx, st);
+    if (rc)
+        return rc;
+    rc = ensure_workspace(ctx, n, st);
     if (rc)
         return rc;
     Workspace &w = ctx->ws;
@@ -2876,8 +2887,12 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     const uint64_t out_bytes = opt_out_bytes(opts);
     hipStream_t st = (hipStream_t) stream;
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    set_last(ctx, st);
-    int rc = ensure_workspace(ctx, n, st);
+    // the workspace and the call state are shared with the ctx's other
+    // streams: this call runs after the work queued on the last one
+    int rc = order_after_last(ctx, st);
+    if (rc)
+        return rc;
+    rc = ensure_workspace(ctx, n, st);
     if (rc)
         return rc;
     Workspace &w = ctx->ws;
@@ -3699,13 +3714,25 @@ int zmqg_fence_record_notify(zmqg_ctx *ctx, void *stream, int fd, uint64_t *fenc
     return 0;
 }
 
+// Wait for the notifications queued on the ctx, at most ~10 s: a stream that
+// never reaches its host function (a stuck kernel, a stream error) leaves
+// -ETIMEDOUT instead of a hang; the caller must then keep the eventfd open.
+static int notify_wait(zmqg_ctx *ctx)
+{
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    while (ctx->notify_pending.load(std::memory_order_acquire) > 0) {
+        if (std::chrono::steady_clock::now() > t_end)
+            return -ETIMEDOUT;
+        sched_yield();
+    }
+    return 0;
+}
+
 int zmqg_notify_quiesce(zmqg_ctx *ctx)
 {
     if (!ctx)
         return -EINVAL;
-    while (ctx->notify_pending.load(std::memory_order_acquire) > 0)
-        sched_yield();
-    return 0;
+    return notify_wait(ctx);
 }
 
 // whether fence `id` has been marked reached by its notification (and

@@ -274,17 +274,27 @@ int curve_batcher_t::launch (slot_t *s)
                                    s->status, &o, _stream);
     }
     const uint64_t t1 = mono_ns ();
+    uint64_t fence = 0;
     if (rc == 0)
         rc = _config.notify_fd >= 0
                ? zmqg_fence_record_notify (_ctx, _stream, _config.notify_fd,
-                                           &s->fence)
-               : zmqg_fence_record (_ctx, _stream, &s->fence);
+                                           &fence)
+               : zmqg_fence_record (_ctx, _stream, &fence);
     if (rc != 0) {
-        //  the slot's messages are lost with the device; keep the slot
-        _free.push_back (s);
+        //  The slot's messages are lost with the device, but kernels of the
+        //  batch may have been queued and still read or write the slot: it
+        //  goes back to the free list only once the stream is known to have
+        //  passed them (its own fence, or a plain one recorded now); when
+        //  that cannot be known the slot leaves the rotation.
+        if (fence == 0 && zmqg_fence_record (_ctx, _stream, &fence) != 0)
+            fence = 0;
+        if (fence != 0 && zmqg_fence_wait (_ctx, fence) == 0)
+            _free.push_back (s);
+        s->n = 0;
         errno = -rc;
         return -1;
     }
+    s->fence = fence;
     _flight.push_back (s);
     _stats.batch_ns += t1 - t0;
     _stats.fence_ns += mono_ns () - t1;

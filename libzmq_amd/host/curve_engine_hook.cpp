@@ -66,10 +66,12 @@ curve_io_hook_t::curve_io_hook_t (zmqg_ctx *ctx_,
 
 curve_io_hook_t::~curve_io_hook_t ()
 {
-    //  the slots' notifications write _fd: it stays open until they ran
+    //  the slots' notifications write _fd: it stays open until they ran (and
+    //  open for good when the ctx cannot tell: a stream that never reaches
+    //  them must not write into a descriptor number reused by then)
     _batcher.wait_idle ();
-    if (_ctx)
-        zmqg_notify_quiesce (_ctx);
+    if (_ctx && zmqg_notify_quiesce (_ctx) != 0)
+        return;
     if (_fd >= 0)
         close (_fd);
 }
