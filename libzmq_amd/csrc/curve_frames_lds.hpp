@@ -66,6 +66,9 @@ namespace zmqg {
         if (ZMQG_LDS_PRIO)                                                                             \
             __builtin_amdgcn_s_setprio(lv);                                                            \
     } while (0)
+#ifndef ZMQG_LDS_ALIGN64
+#define ZMQG_LDS_ALIGN64 1 // cooperative stores as 64-byte-aligned pieces (0: the windows' own granules)
+#endif
 #ifndef ZMQG_LDS_INBUF
 #define ZMQG_LDS_INBUF 2 // input buffers per wave (1: refilled right after it is read)
 #endif
@@ -314,22 +317,65 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
             llim[j] = (uint32_t) __shfl((int) lim, (int) f);
         }
     }
+    // Encode into back-to-back frames (every lane's frame processed, at least
+    // 80 stream bytes, all of the wave's length in windows, each starting
+    // where the lane before's ends: packed
+    // wire output, wave-uniform): the granule a frame boundary falls in is
+    // written whole, once, by the later frame's lane at the end (its wire
+    // bytes 0..15 after the earlier frame's last bytes, read from that
+    // lane's ring), and so are the 16-byte granules of the header, nonce,
+    // tag and first ciphertext bytes -- the cooperative stores cover only
+    // whole granules, and no byte-exact edge stores remain but the wave's
+    // own two ends (without this, an encode wave issued ~3x the store
+    // instructions of a decode wave, and partial granules cost write traffic
+    // beyond the wire bytes: DESIGN.md section 3.1).
+    bool merge = false;
+    uint32_t pend = 0; // merge: ring-relative end (ub + S) of the lane before's frame
+    if (!DEC) {
+        const uint32_t pl = lane ? lane - 1u : 0u;
+        const uint64_t Bp = shfl_u64(B, pl);
+        const uint32_t Sp = (uint32_t) __shfl((int) S, (int) pl);
+        pend = ((uint32_t) Bp & (kStSector - 1u)) + Sp;
+        // (every frame's last window the wave's last: a lane past its frame
+        // would overwrite its ring, and the tail read below, with later steps)
+        const bool ok = valid && S >= 80u && nw == steps && (lane == 0 || Bp + Sp == B);
+        merge = kStSector == 16 && __builtin_amdgcn_ballot_w64(!ok) == 0;
+    }
     // store pair j: granule lane % 4 of frame 16j + lane / 4 of each window; its
     // frame's cooperatively stored bytes are ring-relative [slo, shi) (decode:
-    // the payload, stream bytes 33..S; encode: the ciphertext, 32..S)
+    // the payload, stream bytes 33..S; encode: the ciphertext, 32..S; merged
+    // encode: the whole granules inside it, and the last lane's tail)
+    // Each step stores one 64-byte piece of each frame that is 64-byte
+    // aligned in memory: ring-relative [64u + sh, +64) at step u + 1, sh = 0
+    // when the frame's base granule is 64-byte aligned, else sh = d - 64 with
+    // d the ring offset of the first 64-byte boundary (16, 32 or 48) when d >
+    // ub (the piece then ends inside the window before the one just computed)
+    // -- whole 64-byte segments, so no segment is written in two halves by
+    // two steps (WRITE_SIZE counted those twice: 1.5-1.7x the bytes).  The
+    // ring holds ring-relative granule r at r mod 128 for the two windows it
+    // keeps (the spill copy keeps that true across the odd windows' overflow).
     uint64_t sa[4];
     uint32_t sro[4], slo4[4], shi4[4];
+    int32_t ssh4[4];
     const uint32_t srel = 16u * (lane & 3u);
     {
         const uint64_t Gb = B - ub;
-        const uint32_t slo = ub + (DEC ? 33u : 32u), shi = S ? ub + S : 0u;
+        const uint32_t d = (64u - ((uint32_t) Gb & 63u)) & 63u;
+        const int32_t sh = ZMQG_LDS_ALIGN64 && d > ub ? (int32_t) d - 64 : 0;
+        uint32_t slo = ub + (DEC ? 33u : 32u), shi = S ? ub + S : 0u;
+        if (merge) {
+            slo = (slo + 15u) & ~15u;
+            if (lane != 63u)
+                shi &= ~15u;
+        }
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t f = 16u * j + (lane >> 2);
             sa[j] = shfl_u64(Gb, f) + srel;
-            sro[j] = kStRing * f + srel;
+            sro[j] = kStRing * f;
             slo4[j] = (uint32_t) __shfl((int) slo, (int) f);
             shi4[j] = (uint32_t) __shfl((int) shi, (int) f);
+            ssh4[j] = __shfl(sh, (int) f);
         }
     }
     // window t's input cover -> input buffer t & 1 (no wait)
@@ -344,29 +390,36 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     };
     // window t's output granules from the ring: the four reads first, then
     // the whole granules, then (rarely, a wave-uniform branch) the partial ones
+    // piece t's granules (ring-relative 64t + sh + 16 (lane % 4)); a piece
+    // before the frame's first byte (t = 0 with sh < 0) stores nothing
     auto ring_get = [&](uint32_t t, u32x4 (&g)[4]) {
-        const uint32_t half = 64u * (t & 1u);
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            g[j] = *(const u32x4 *) (ring + sro[j] + half);
+        for (uint32_t j = 0; j < 4; ++j) {
+            const int32_t r = (int32_t) (64u * t + srel) + ssh4[j];
+            g[j] = *(const u32x4 *) (ring + sro[j] + ((uint32_t) r & 127u));
+        }
     };
     auto ring_store = [&](uint32_t t, const u32x4 (&g)[4]) {
-        const uint32_t r = 64u * t + srel;
         uint32_t partm = 0;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
-            const bool full = r >= slo4[j] && r + 16u <= shi4[j];
-            const bool part = !full && r < shi4[j] && r + 16u > slo4[j];
+            const int32_t rs = (int32_t) (64u * t + srel) + ssh4[j];
+            const uint32_t r = (uint32_t) rs;
+            const bool in = rs >= 0;
+            const bool full = in && r >= slo4[j] && r + 16u <= shi4[j];
+            const bool part = in && !full && r < shi4[j] && r + 16u > slo4[j];
             if (full)
-                *(GU4 *) (uintptr_t) (sa[j] + 64ull * t) = g[j];
+                *(GU4 *) (uintptr_t) (sa[j] + (int64_t) (64 * (int32_t) t + ssh4[j])) = g[j];
             partm |= part ? 1u << j : 0u;
         }
         if (!(ZMQG_FRAMES_ABLATE & 512) && __builtin_amdgcn_ballot_w64(partm != 0) != 0) {
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
-                if ((partm >> j) & 1u)
-                    granule_store_part(sa[j] + 64ull * t, slo4[j] > r ? slo4[j] - r : 0u,
+                if ((partm >> j) & 1u) {
+                    const uint32_t r = (uint32_t) ((int32_t) (64u * t + srel) + ssh4[j]);
+                    granule_store_part(sa[j] + (int64_t) (64 * (int32_t) t + ssh4[j]), slo4[j] > r ? slo4[j] - r : 0u,
                                        shi4[j] - r < 16u ? shi4[j] - r : 16u, g[j]);
+                }
         }
     };
     auto store_window_t = [&](uint32_t t) {
@@ -403,6 +456,7 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     uint32_t spad[4], wtag[4] = {0, 0, 0, 0}, fl = 0;
     uint32_t cp[16];                // ciphertext of the window whose MAC is absorbed next step
     uint32_t cp_j0 = 2, cp_len = 0; // its first block slot and ciphertext bytes
+    uint32_t ct0[4];                // merged encode: ciphertext bytes 0..15 (wire 32..47)
     {
         uint32_t ks[16];
         salsa20_block(ks, key, n0, n1, 0, 0);
@@ -446,6 +500,9 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
         for (int k = 0; k < 16; ++k)
             cp[k] = DEC ? x[k] : y[k];
         cp_len = (S < 64u ? S : 64u) - 32u; // (S = 0: unused)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            ct0[k] = y[8 + k];
         if (DEC)
             fl = y[8] & 3u;
         // stream bytes 0..31 (decode: header/nonce/tag; encode: the Poly1305
@@ -605,7 +662,48 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
     }
     uint32_t tag[4];
     poly32_finish(h, spad, tag);
-    if (!DEC) {
+    if (!DEC && merge) {
+        // wire bytes 0..47 ("\x07MESSAGE", nonce, tag, ciphertext 0..15) laid
+        // out at the frame's byte offset ub in the granules [G, G + 48)
+        const uint32_t o[12] = {0x53454d07u, 0x45474153u, n0,     n1,     tag[0], tag[1],
+                                tag[2],      tag[3],      ct0[0], ct0[1], ct0[2], ct0[3]};
+        const uint32_t m0 = ub >> 2, sb = ub & 3u;
+        uint32_t gw[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            // (compile-time indices for each word shift; ub picks one)
+            const uint32_t h0 = o[j], l0 = j >= 1 ? o[j - 1] : 0u;
+            const uint32_t h1 = j >= 1 ? o[j - 1] : 0u, l1 = j >= 2 ? o[j - 2] : 0u;
+            const uint32_t h2 = j >= 2 ? o[j - 2] : 0u, l2 = j >= 3 ? o[j - 3] : 0u;
+            const uint32_t h3 = j >= 3 ? o[j - 3] : 0u, l3 = j >= 4 ? o[j - 4] : 0u;
+            const uint32_t hi = m0 == 0 ? h0 : m0 == 1 ? h1 : m0 == 2 ? h2 : h3;
+            const uint32_t lo = m0 == 0 ? l0 : m0 == 1 ? l1 : m0 == 2 ? l2 : l3;
+            gw[j] = sb == 0 ? hi : __builtin_amdgcn_alignbyte(hi, lo, 4u - sb);
+        }
+        const uint64_t G = B - ub;
+        u32x4 g0 = {gw[0], gw[1], gw[2], gw[3]};
+        if (ub != 0 && lane != 0) {
+            // the granule's first ub bytes: the end of the lane before's frame,
+            // in its ring at that frame's granule (pend >> 4) mod 8
+            const u32x4 pg = *(const u32x4 *) (ring + kStRing * (lane - 1u) + 16u * ((pend >> 4) & 7u));
+            const uint32_t pw[4] = {pg.x, pg.y, pg.z, pg.w};
+            uint32_t mw[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const int nb = (int) ub - 4 * (int) j; // bytes of word j from the lane before
+                const uint32_t mask = nb >= 4 ? 0xffffffffu : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+                mw[j] = (pw[j] & mask) | (gw[j] & ~mask);
+            }
+            g0 = (u32x4){mw[0], mw[1], mw[2], mw[3]};
+        }
+        if (ub == 0 || lane != 0)
+            *(GU4 *) (uintptr_t) G = g0;
+        else
+            granule_store_part(G, ub, 16u, g0);
+        *(GU4 *) (uintptr_t) (G + 16u) = (u32x4){gw[4], gw[5], gw[6], gw[7]};
+        if (ub != 0)
+            *(GU4 *) (uintptr_t) (G + 32u) = (u32x4){gw[8], gw[9], gw[10], gw[11]};
+    } else if (!DEC) {
         // "\x07MESSAGE" || nonce || tag: wire bytes 0..31 (the rest went out cooperatively)
         uint32_t o[16] = {0x53454d07u, 0x45474153u, n0, n1, tag[0], tag[1], tag[2], tag[3]};
         if (ZMQG_FRAMES_ABLATE & 1024) { // (timing only: two aligned dwordx4 at the granule below)

@@ -7,7 +7,7 @@ for c in ${CFGS:-3 4 5}; do
   O=gpurun_out/cfgprof/c$c
   mkdir -p $O
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O -o run -- \
-      python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-staged --configs $c > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
+      python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-staged --no-deployable --hbm-sets 0 --configs $c > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
   python - "$O" "$c" <<'PY'
 import csv, glob, json, sys
 o, c = sys.argv[1], sys.argv[2]
