@@ -658,7 +658,7 @@ def config_step(b):
                           max_len=b["bound"] + 33 if b["bound"] else 0)
 
 
-def other_configs(C, torch, dev, local, rank, world, which, steps=3, warmup=1, settle_ms=40.0):
+def other_configs(C, torch, dev, local, rank, world, which, steps=10, warmup=1, settle_ms=40.0):
     """BASELINE configs 3, 4, 5: encode (device-assigned nonces) + decode round
     trips of device-resident batches, every result checked, timed like the
     main line (barrier + synchronize, max over ranks); payload GiB/s of the
