@@ -183,23 +183,17 @@ __device__ __forceinline__ uint64_t zmtp_block_excl4(uint64_t v, uint64_t &total
     return base + x - v;
 }
 
-__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, uint64_t n, int64_t max_msg,
-                                                            uint64_t *cand_wg, uint64_t *count_wg)
+// Chunk (k, thread) = stream bytes [t0 + 16 (256 k + thread), +16) of the tile
+// t0 = 16 KiB x tile, k = 0..3: consecutive lanes read consecutive chunks
+// (coalesced), each with the 16 bytes before it (a header) and the 8 after (a
+// signature's tail), so the signature and header tests run on registers.
+constexpr uint32_t kZmtpRounds = kZmtpWgBytes / 16u / kZmtpThreads; // 4
+__device__ __forceinline__ void zmtp_scan_load(const uint8_t *b, uint64_t n, uint64_t tile,
+                                               uint32_t (&w)[kZmtpRounds][10])
 {
-    // Chunk (k, thread) = stream bytes [wg0 + 16 (256 k + thread), +16), k =
-    // 0..3: consecutive lanes read consecutive chunks (coalesced), each with
-    // the 16 bytes before it (a header) and the 8 after (a signature's tail),
-    // so the signature and header tests run on registers.  All four rounds'
-    // loads go out first; candidates go out in (k, thread) order, which is
-    // stream order, after one block scan of the four rounds' counts packed in
-    // 16-bit fields (a workgroup holds at most kZmtpWgCap = 2048 of them).
-    constexpr uint32_t R = kZmtpWgBytes / 16u / kZmtpThreads; // 4 rounds
-    static_assert(R == 4, "four 16-bit count fields");
-    const uint64_t wg0 = (uint64_t) blockIdx.x * kZmtpWgBytes;
-    uint64_t *const dst0 = cand_wg + (size_t) blockIdx.x * kZmtpWgCap;
-    uint32_t w[R][10]; // round k: stream bytes [base_k - 16, base_k + 24), zero outside [0, n)
+    const uint64_t wg0 = tile * kZmtpWgBytes;
 #pragma unroll
-    for (uint32_t k = 0; k < R; ++k) {
+    for (uint32_t k = 0; k < kZmtpRounds; ++k) {
         const uint64_t base = wg0 + 16ull * (k * kZmtpThreads + threadIdx.x);
         if (base >= 16 && base + 24 <= n) {
             const uint4 v0 = *(const uint4 *) (b + base - 16);
@@ -227,6 +221,19 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
             }
         }
     }
+}
+
+// One tile's candidates from its registers: written in (k, thread) order,
+// which is stream order, after one block scan of the four rounds' counts
+// packed in 16-bit fields (a tile holds at most kZmtpWgCap = 2048 of them).
+__device__ __forceinline__ void zmtp_scan_tile(uint64_t n, int64_t max_msg, uint64_t tile,
+                                               const uint32_t (&w)[kZmtpRounds][10], uint64_t *cand_wg,
+                                               uint64_t *count_wg, uint16_t *count16)
+{
+    constexpr uint32_t R = kZmtpRounds;
+    static_assert(R == 4, "four 16-bit count fields");
+    const uint64_t wg0 = tile * kZmtpWgBytes;
+    uint64_t *const dst0 = cand_wg + (size_t) tile * kZmtpWgCap;
     uint64_t f[R][2]; // (at most 2 per chunk: signatures are >= 8 bytes apart)
     uint32_t cnt[R];
 #pragma unroll
@@ -282,59 +289,183 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, ui
             dst0[off + 1] = f[k][1];
         base_out += (uint32_t) ((tot >> (16 * k)) & 0xffffu);
     }
-    if (threadIdx.x == 0)
-        count_wg[blockIdx.x] = base_out;
+    if (threadIdx.x == 0) {
+        count_wg[tile] = base_out;
+        count16[tile] = (uint16_t) base_out; // (<= kZmtpWgCap = 2048)
+    }
 }
 
-// Workgroup lists -> the sorted candidate array (off_wg: exclusive sum of the
-// counts, off_wg[nwg] = m), and the links (round 4: in this kernel, no launch
-// of their own): candidate k is unlinked when its frame does not end at
-// candidate k+1 (the last one never does).  k+1 is the next entry of the same
-// list, or the first entry of the next non-empty list (found from the
-// counts), so no other workgroup's output of this launch is needed.  Per list: nb[k] =
-// the first unlinked index >= k in k's list (or none), first_w[w] = the first
-// unlinked index of list w (or none), wid[k] = w.
-__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint8_t *b, uint64_t n, const uint64_t *cand_wg,
-                                                               const uint64_t *count_wg, const uint64_t *off_wg,
-                                                               uint32_t nwg, uint64_t *cand,
-                                                               uint64_t *nb, uint64_t *first_w, uint32_t *wid)
+// Candidate scan, one workgroup per tile.
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan(const uint8_t *b, uint64_t n, int64_t max_msg,
+                                                            uint64_t *cand_wg, uint64_t *count_wg,
+                                                            uint16_t *count16)
 {
-    __shared__ unsigned long long sh[kZmtpThreads / 64];
-    const uint32_t w = blockIdx.x, c = (uint32_t) count_wg[w], tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wv = tid >> 6;
-    const uint64_t o = off_wg[w];
-    const uint64_t *const list = cand_wg + (size_t) w * kZmtpWgCap;
-    // the first entry of the next non-empty list: the workgroup looks at the
-    // next 256 lists' counts at once (further only behind a 4 MiB gap)
-    __shared__ uint32_t sh_nx[kZmtpThreads / 64];
-    uint64_t after = kZmtpNone;
-    for (uint32_t w0 = w + 1; c > 0 && w0 < nwg; w0 += kZmtpThreads) {
-        const uint32_t q = w0 + tid;
-        const unsigned long long nz = __ballot(q < nwg && count_wg[q] != 0);
+    uint32_t w[kZmtpRounds][10];
+    zmtp_scan_load(b, n, blockIdx.x, w);
+    zmtp_scan_tile(n, max_msg, blockIdx.x, w, cand_wg, count_wg, count16);
+}
+
+// The same as a persistent grid: each workgroup takes tiles blockIdx.x,
+// + gridDim.x, ..., the next tile's loads in flight while it tests the
+// current one.
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_scan_p(const uint8_t *b, uint64_t n, int64_t max_msg,
+                                                              uint64_t nwg, uint64_t *cand_wg, uint64_t *count_wg,
+                                                              uint16_t *count16)
+{
+    uint32_t wa[kZmtpRounds][10], wb[kZmtpRounds][10];
+    uint64_t t = blockIdx.x;
+    if (t >= nwg)
+        return;
+    zmtp_scan_load(b, n, t, wa);
+    for (;;) {
+        const uint64_t tn = t + gridDim.x;
+        if (tn < nwg)
+            zmtp_scan_load(b, n, tn, wb);
+        zmtp_scan_tile(n, max_msg, t, wa, cand_wg, count_wg, count16);
+        if (tn >= nwg)
+            break;
+        __syncthreads(); // (the block scan's LDS is reused)
+        t = tn;
+        const uint64_t tn2 = t + gridDim.x;
+        if (tn2 < nwg)
+            zmtp_scan_load(b, n, tn2, wa);
+        zmtp_scan_tile(n, max_msg, t, wb, cand_wg, count_wg, count16);
+        if (tn2 >= nwg)
+            break;
         __syncthreads();
+        t = tn2;
+    }
+}
+
+// A candidate's header (it passed the scan's tests: header and body lie inside
+// [0, n)): its nine bytes loaded at once, not the flags byte first; returns
+// the flags byte.
+__device__ __forceinline__ uint32_t zmtp_cand_header(const uint8_t *b, uint64_t n, uint64_t p, uint32_t &hdr,
+                                                     uint64_t &size)
+{
+    if (p + 9 <= n) {
+        uint32_t x[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            x[k] = b[p + k];
+        if (x[0] & kZmtpLarge) {
+            uint64_t v = 0;
+#pragma unroll
+            for (int k = 1; k <= 8; ++k)
+                v = (v << 8) | x[k];
+            hdr = 9;
+            size = v;
+        } else {
+            hdr = 2;
+            size = x[1];
+        }
+        return x[0];
+    }
+    zmtp_header(b, n, p, hdr, size);
+    return b[p];
+}
+
+// Tile lists -> the sorted candidate array, and the links (round 4: in this
+// kernel, no launch of their own): candidate k is unlinked when its frame
+// does not end at candidate k+1 (the last one never does).  k+1 is the next
+// entry of the same list, or the first entry of the next non-empty list
+// (found from the counts), so no other list's output of this launch is
+// needed.  Per list: nb[k] = the first unlinked index >= k in k's list (or
+// none), first_w[w] = the first unlinked index of list w (or none), wid[k] = w;
+// per candidate also its frame (cdesc[k] = body offset | body length << 32,
+// cflag[k] = the flags byte), so the walk and the descriptors read no header.
+// One wave per list, four lists a workgroup (round 6: a workgroup per list
+// kept 4,266 workgroups of mostly idle lanes in flight for the config-2
+// stream -- ~16 candidates a list -- behind four barriers each; 12.3 us).
+// The list's place in the array: with count16, the sum of the counts before
+// it, taken here (round 6: the separate one-workgroup sum kernel cost ~5 us
+// of launch and dependent latency): the workgroup sums the counts before its
+// first list (a few 16-byte loads per thread, L2-resident), each wave adds
+// the lists of its workgroup before its own, and the wave of the last list
+// writes the candidate count to off_wg[nwg]; without count16 (large streams),
+// off_wg holds the exclusive sum already.
+// Latency: every load that depends on nothing else (the list's count and
+// first 65 entries, the next 64 lists' counts, the counts to sum) goes out
+// first; the next list's first entry and the headers are the second and
+// last round of dependent loads (round 5 had seven).
+constexpr uint32_t kZmtpCompactLists = kZmtpThreads / 64; // lists per workgroup
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint8_t *b, uint64_t n, const uint64_t *cand_wg,
+                                                               const uint64_t *count_wg, const uint16_t *count16,
+                                                               uint64_t *off_wg, uint32_t nwg, uint64_t *cand,
+                                                               uint64_t *cdesc, uint8_t *cflag, uint64_t *nb,
+                                                               uint64_t *first_w, uint32_t *wid)
+{
+    __shared__ uint32_t sh_o[kZmtpThreads / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t w0 = blockIdx.x * kZmtpCompactLists, w = w0 + wv;
+    const bool live = w < nwg; // (the wave of a list past the end only helps with the sum)
+    const uint32_t wl = live ? w : nwg - 1;
+    const uint64_t *const list = cand_wg + (size_t) wl * kZmtpWgCap;
+    // round 1 of loads
+    const uint32_t c = live ? (uint32_t) count_wg[wl] : 0u;
+    const uint64_t p0 = list[lane], p1 = list[lane + 1]; // chunk 0 (entries past c unused)
+    uint32_t q = w + 1 + lane;
+    bool nz = q < nwg && count_wg[q] != 0;
+    uint64_t o;
+    if (count16) {
+        // the lists before w0 (summed by the whole workgroup) and this
+        // wave's predecessors in the workgroup, w0 .. w - 1 (by the wave)
+        uint32_t pb = lane < wv && w0 + lane < nwg ? count16[w0 + lane] : 0u;
+        uint32_t s = 0;
+        const uint32_t w8 = w0 & ~7u;
+        for (uint32_t i = tid * 8u; i < w8; i += kZmtpThreads * 8u) {
+            const uint4 v = *(const uint4 *) (count16 + i);
+            s += (v.x & 0xffffu) + (v.x >> 16) + (v.y & 0xffffu) + (v.y >> 16) + (v.z & 0xffffu) + (v.z >> 16) +
+                 (v.w & 0xffffu) + (v.w >> 16);
+        }
+        if (tid < (w0 & 7u))
+            s += count16[w8 + tid];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            s += __shfl_xor(s, d);
+            pb += __shfl_xor(pb, d);
+        }
         if (lane == 0)
-            sh_nx[wv] = nz ? w0 + 64u * wv + (uint32_t) __builtin_ctzll(nz) : nwg;
+            sh_o[wv] = s;
         __syncthreads();
-        uint32_t f = nwg;
+        o = pb;
+#pragma unroll
         for (uint32_t k = 0; k < kZmtpThreads / 64; ++k)
-            f = sh_nx[k] < f ? sh_nx[k] : f;
-        if (f < nwg) {
-            after = cand_wg[(size_t) f * kZmtpWgCap];
+            o += sh_o[k];
+        if (live && w + 1 == nwg && lane == 0)
+            off_wg[nwg] = o + c;
+    } else {
+        o = live ? off_wg[wl] : 0;
+    }
+    if (!live)
+        return;
+    // the first entry of the next non-empty list (further than the next 64
+    // lists only behind a 1 MiB gap)
+    uint64_t after = kZmtpNone;
+    for (uint32_t ws = w + 1; c > 0 && ws < nwg;) {
+        const unsigned long long bal = __ballot(nz);
+        if (bal) {
+            after = cand_wg[(size_t) (ws + (uint32_t) __builtin_ctzll(bal)) * kZmtpWgCap];
             break;
         }
+        ws += 64u;
+        q = ws + lane;
+        nz = q < nwg && count_wg[q] != 0;
     }
     unsigned long long carry = kZmtpNone; // the minimum over the later chunks
-    for (int j = (int) ((c + kZmtpThreads - 1) / kZmtpThreads) - 1; j >= 0; --j) {
-        const uint32_t k = (uint32_t) j * kZmtpThreads + tid;
+    for (int j = (int) ((c + 63u) / 64u) - 1; j >= 0; --j) {
+        const uint32_t k = (uint32_t) j * 64u + lane;
         unsigned long long u = kZmtpNone;
         if (k < c) {
-            const uint64_t p = list[k];
-            cand[o + k] = p;
-            wid[o + k] = w;
-            const uint64_t next = k + 1 < c ? list[k + 1] : after;
+            const uint64_t p = j == 0 ? p0 : list[k];
+            const uint64_t next = k + 1 < c ? (j == 0 ? p1 : list[k + 1]) : after;
             uint32_t hdr;
             uint64_t size;
-            zmtp_header(b, n, p, hdr, size);
+            const uint32_t fl = zmtp_cand_header(b, n, p, hdr, size);
+            cand[o + k] = p;
+            wid[o + k] = w;
+            cdesc[o + k] = (p + hdr) | (size << 32); // (in_bytes < 2^31: both fit)
+            cflag[o + k] = (uint8_t) fl;
             u = next != p + hdr + size ? o + k : kZmtpNone;
         }
         // suffix minimum within the chunk, then the later chunks'
@@ -344,22 +475,12 @@ __global__ __launch_bounds__(kZmtpThreads) void k_zmtp_compact(const uint8_t *b,
             if (lane + d < 64u && x < u)
                 u = x;
         }
-        __syncthreads();
-        if (lane == 0)
-            sh[wv] = u;
-        __syncthreads();
-        for (uint32_t q = wv + 1; q < kZmtpThreads / 64; ++q)
-            u = sh[q] < u ? sh[q] : u;
         u = carry < u ? carry : u;
         if (k < c)
             nb[o + k] = u;
-        // the chunk's minimum: wave 0's lane 0 value with the later waves' and chunks'
-        unsigned long long lo = carry;
-        for (uint32_t q = 0; q < kZmtpThreads / 64; ++q)
-            lo = sh[q] < lo ? sh[q] : lo;
-        carry = lo;
+        carry = __shfl(u, 0); // the chunk's minimum with the later chunks'
     }
-    if (tid == 0)
+    if (lane == 0)
         first_w[w] = carry;
 }
 
@@ -370,15 +491,28 @@ constexpr uint32_t kZmtpNextThreads = 1024;
 template <uint32_t T>
 __device__ void zmtp_suffix_min(uint64_t *first_w, uint64_t count)
 {
-    // (wave shuffles, one LDS exchange between the waves)
+    // (wave shuffles, one LDS exchange between the waves; up to 8 entries a
+    // thread -- 8,192 lists -- read once, all loads at once, into registers)
+    constexpr uint32_t R = 8;
     __shared__ unsigned long long sh[T / 64];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint64_t per = (count + T - 1) / T;
     const uint64_t r0 = threadIdx.x * per < count ? threadIdx.x * per : count;
     const uint64_t r1 = r0 + per < count ? r0 + per : count;
+    const bool regs = per <= R;
+    unsigned long long v[R];
     unsigned long long x = kZmtpNone;
-    for (uint64_t s = r0; s < r1; ++s)
-        x = first_w[s] < x ? first_w[s] : x;
+    if (regs) {
+#pragma unroll
+        for (uint32_t i = 0; i < R; ++i)
+            v[i] = r0 + i < r1 ? first_w[r0 + i] : kZmtpNone;
+#pragma unroll
+        for (uint32_t i = 0; i < R; ++i)
+            x = v[i] < x ? v[i] : x;
+    } else {
+        for (uint64_t s = r0; s < r1; ++s)
+            x = first_w[s] < x ? first_w[s] : x;
+    }
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const unsigned long long y = __shfl_down(x, d);
@@ -393,49 +527,25 @@ __device__ void zmtp_suffix_min(uint64_t *first_w, uint64_t count)
         later = sh[q] < later ? sh[q] : later;
     const unsigned long long nx = __shfl_down(x, 1);
     unsigned long long c = lane < 63u ? (nx < later ? nx : later) : later; // minimum over the later threads
-    for (uint64_t s = r1; s-- > r0;) {
-        const unsigned long long v = first_w[s];
-        c = v < c ? v : c;
-        first_w[s] = c;
+    if (regs) {
+#pragma unroll
+        for (int i = (int) R - 1; i >= 0; --i)
+            if (r0 + i < r1) {
+                c = v[i] < c ? v[i] : c;
+                first_w[r0 + i] = c;
+            }
+    } else {
+        for (uint64_t s = r1; s-- > r0;) {
+            const unsigned long long e = first_w[s];
+            c = e < c ? e : c;
+            first_w[s] = c;
+        }
     }
 }
 
-// Exclusive sum of v[0..n) into o[0..n] (o[n] = total) by one workgroup of
-// 1024 threads, each a contiguous run: the workgroups' candidate counts.
-constexpr uint32_t kZmtpScan1 = 1024;
-__global__ __launch_bounds__(kZmtpScan1) void k_zmtp_exsum(const uint64_t *v, uint64_t n, uint64_t *o)
-{
-    // (wave shuffles, one LDS exchange between the waves)
-    __shared__ unsigned long long sh[kZmtpScan1 / 64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t per = (n + kZmtpScan1 - 1) / kZmtpScan1;
-    const uint64_t r0 = threadIdx.x * per < n ? threadIdx.x * per : n, r1 = r0 + per < n ? r0 + per : n;
-    unsigned long long t = 0;
-    for (uint64_t i = r0; i < r1; ++i)
-        t += v[i];
-    unsigned long long x = t;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long y = __shfl_up(x, d);
-        if ((int) lane >= d)
-            x += y;
-    }
-    if (lane == 63)
-        sh[wv] = x;
-    __syncthreads();
-    unsigned long long acc = x - t, tot = 0;
-    for (uint32_t q = 0; q < kZmtpScan1 / 64; ++q) {
-        acc += q < wv ? sh[q] : 0ull;
-        tot += sh[q];
-    }
-    for (uint64_t i = r0; i < r1; ++i) {
-        const unsigned long long y = v[i];
-        o[i] = acc;
-        acc += y;
-    }
-    if (threadIdx.x == 0)
-        o[n] = tot;
-}
+// Streams up to this many 16 KiB lists (128 MiB) take their offsets inside
+// k_zmtp_compact; longer ones from a hipCUB scan of the counts.
+constexpr uint32_t kZmtpInlineSumLists = 8192;
 
 // Parse state written by k_zmtp_walk (device).  It begins with the call's
 // result (zmqg_zmtp_result's layout), which the decode's frame kernel copies
@@ -455,20 +565,27 @@ static_assert(sizeof(zmqg_zmtp_result) == 32 && offsetof(ZmtpWalk, runs) == 32, 
 // Thread 0 walks the chain (see the file comment).  run[2r], run[2r+1]: the
 // first and last candidate of run r; runpre[r]: frames before run r.  The
 // next unlinked candidate >= cur is nb[cur], or (none left in cur's list
-// wid[cur]) first_w[wid[cur] + 1], already a suffix minimum over the lists.
+// wid[cur]) first_w[wid[cur] + 1], already a suffix minimum over the lists;
+// a frame's end comes from cdesc.  pre: what the walk reads first (m, cand[0],
+// nb[0], wid[0], cdesc[m - 1]), loaded before the suffix minimum's barrier;
+// the clean stream's walk is then one more load (first_w[1]).
+struct ZmtpWalkPre {
+    uint64_t m, cand0, nb0, dlast;
+    uint32_t wid0;
+};
 __device__ void zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_t max_frames, const uint64_t *cand,
-                          const uint64_t *m_p, const uint64_t *nb, const uint64_t *first_w, const uint32_t *wid,
-                          uint64_t nwg, uint64_t *run, uint64_t *runpre, ZmtpWalk *out)
+                          const uint64_t *cdesc, const ZmtpWalkPre &pre, const uint64_t *nb, const uint64_t *first_w,
+                          const uint32_t *wid, uint64_t nwg, uint64_t *run, uint64_t *runpre, ZmtpWalk *out)
 {
-    const uint64_t m = *m_p;
+    const uint64_t m = pre.m;
     uint64_t frames = 0, runs = 0, q = 0;
     bool full = false;
-    if (m > 0 && cand[0] == 0 && max_frames > 0) {
+    if (m > 0 && pre.cand0 == 0 && max_frames > 0) {
         uint64_t cur = 0;
         for (;;) {
-            uint64_t last = nb[cur];
+            uint64_t last = cur ? nb[cur] : pre.nb0;
             if (last == kZmtpNone) {
-                const uint64_t wn = (uint64_t) wid[cur] + 1u;
+                const uint64_t wn = (uint64_t) (cur ? wid[cur] : pre.wid0) + 1u;
                 last = wn < nwg ? first_w[wn] : kZmtpNone;
             }
             if (last == kZmtpNone)
@@ -482,10 +599,8 @@ __device__ void zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_
             runpre[runs] = frames;
             ++runs;
             frames += last - cur + 1;
-            uint32_t hdr;
-            uint64_t size;
-            zmtp_header(b, n, cand[last], hdr, size);
-            q = cand[last] + hdr + size;
+            const uint64_t d = last == m - 1 ? pre.dlast : cdesc[last];
+            q = (d & 0xffffffffull) + (d >> 32); // the frame's end
             if (full)
                 break;
             // the next frame starts at q: a candidate further on, or the end
@@ -529,24 +644,34 @@ __device__ void zmtp_walk(const uint8_t *b, uint64_t n, int64_t max_msg, uint64_
 // first_w's suffix minimum over the lists, then thread 0 walks.
 __global__ __launch_bounds__(kZmtpNextThreads) void k_zmtp_next_walk(const uint8_t *b, uint64_t n, int64_t max_msg,
                                                                      uint64_t max_frames, const uint64_t *cand,
-                                                                     const uint64_t *m_p, const uint64_t *nb,
-                                                                     uint64_t *first_w, const uint32_t *wid,
-                                                                     uint64_t nwg, uint64_t *run, uint64_t *runpre,
-                                                                     ZmtpWalk *out)
+                                                                     const uint64_t *cdesc, const uint64_t *m_p,
+                                                                     const uint64_t *nb, uint64_t *first_w,
+                                                                     const uint32_t *wid, uint64_t nwg, uint64_t *run,
+                                                                     uint64_t *runpre, ZmtpWalk *out)
 {
+    ZmtpWalkPre pre{};
+    if (threadIdx.x == 0) {
+        // (index 0 is read even when there are no candidates: the arrays
+        // always hold at least 1,024 entries, and m = 0 ignores them)
+        pre.m = *m_p;
+        pre.cand0 = cand[0];
+        pre.nb0 = nb[0];
+        pre.wid0 = wid[0];
+        pre.dlast = pre.m ? cdesc[pre.m - 1] : 0;
+    }
     zmtp_suffix_min<kZmtpNextThreads>(first_w, nwg);
     __threadfence_block();
     __syncthreads();
     if (threadIdx.x == 0)
-        zmtp_walk(b, n, max_msg, max_frames, cand, m_p, nb, first_w, wid, nwg, run, runpre, out);
+        zmtp_walk(b, n, max_msg, max_frames, cand, cdesc, pre, nb, first_w, wid, nwg, run, runpre, out);
 }
 
 // Frame descriptors from the runs (a persistent grid over the candidates).  Entries [frames, max_frames) get an empty frame
 // (offset 0, length 0: the decode reports it malformed and writes nothing
 // else), so the decode can run over max_frames without the frame count
 // reaching the host.
-__device__ __forceinline__ void zmtp_frames_body(const uint8_t *b, uint64_t n, const uint64_t *cand, uint64_t m,
-                                                 const uint64_t *run, const uint64_t *runpre, const ZmtpWalk *walk,
+__device__ __forceinline__ void zmtp_frames_body(const uint8_t *b, uint64_t n, const uint64_t *cdesc,
+                                                 const uint8_t *cflag, uint64_t m, const uint64_t *run, const uint64_t *runpre, const ZmtpWalk *walk,
                                                  uint64_t max_frames, uint64_t *f_off, uint32_t *f_len,
                                                  uint8_t *f_flags, uint32_t *sid_fill, uint32_t sid,
                                                  uint64_t *out_off, unsigned long long *out_bytes, bool pad)
@@ -578,6 +703,8 @@ __device__ __forceinline__ void zmtp_frames_body(const uint8_t *b, uint64_t n, c
         pb += size >= 33u ? size - 33u : 0u;
     }
     for (uint64_t k = (uint64_t) blockIdx.x * kZmtpThreads + threadIdx.x; runs > 0 && k < m; k += stride) {
+        const uint64_t d = cdesc[k]; // (loaded before the runs are searched)
+        const uint8_t fl = cflag[k];
         // the run holding k: last run whose first candidate <= k
         uint64_t lo = 0, hi = runs;
         while (hi - lo > 1) {
@@ -590,13 +717,11 @@ __device__ __forceinline__ void zmtp_frames_body(const uint8_t *b, uint64_t n, c
         if (k < run[2 * lo] || k > run[2 * lo + 1])
             continue; // not on the chain
         const uint64_t j = runpre[lo] + (k - run[2 * lo]);
-        uint32_t hdr;
-        uint64_t size;
-        zmtp_header(b, n, cand[k], hdr, size);
-        f_off[j] = cand[k] + hdr;
+        const uint64_t body = d & 0xffffffffull, size = d >> 32;
+        f_off[j] = body;
         f_len[j] = (uint32_t) size;
-        f_flags[j] = b[cand[k]];
-        out_off[j] = cand[k] + hdr; // the payload at its body's offset (see zmqg_decode_zmtp)
+        f_flags[j] = fl;
+        out_off[j] = body; // the payload at its body's offset (see zmqg_decode_zmtp)
         pb += size >= 33u ? size - 33u : 0u;
     }
     // the call's payload bytes: one atomic per workgroup (walk->out_bytes
@@ -616,14 +741,15 @@ __device__ __forceinline__ void zmtp_frames_body(const uint8_t *b, uint64_t n, c
     }
 }
 
-__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, uint64_t n, const uint64_t *cand,
-                                                              const uint64_t *m_p, const uint64_t *run,
+__global__ __launch_bounds__(kZmtpThreads) void k_zmtp_frames(const uint8_t *b, uint64_t n, const uint64_t *cdesc,
+                                                              const uint8_t *cflag, const uint64_t *m_p,
+                                                              const uint64_t *run,
                                                               const uint64_t *runpre, const ZmtpWalk *walk,
                                                               uint64_t max_frames, uint64_t *f_off, uint32_t *f_len,
                                                               uint8_t *f_flags, uint32_t *sid_fill, uint32_t sid,
                                                               uint64_t *out_off, unsigned long long *out_bytes)
 {
-    zmtp_frames_body(b, n, cand, *m_p, run, runpre, walk, max_frames, f_off, f_len, f_flags, sid_fill, sid, out_off,
+    zmtp_frames_body(b, n, cdesc, cflag, *m_p, run, runpre, walk, max_frames, f_off, f_len, f_flags, sid_fill, sid, out_off,
                      out_bytes, true);
 }
 

@@ -180,7 +180,10 @@ struct ZmtpWs {
     uint64_t *cand_wg = nullptr;          // [g_cap * kZmtpWgCap] each workgroup's candidates, in order
     uint64_t *count_wg = nullptr;         // [g_cap + 1]
     uint64_t *off_wg = nullptr;           // [g_cap + 1] exclusive sum of count_wg
+    uint16_t *count16 = nullptr;          // [g_cap + 8] count_wg as 16-bit fields (k_zmtp_compact sums them)
     uint64_t *cand = nullptr;             // [c_cap] sorted candidates
+    uint64_t *cdesc = nullptr;            // [c_cap] their frames: body offset | body length << 32
+    uint8_t *cflag = nullptr;             // [c_cap] their flags bytes
     uint64_t *nb = nullptr;               // [c_cap] next unlinked candidate in the 256-candidate segment
     uint64_t *first_w = nullptr;          // [g_cap + 1] first unlinked candidate in workgroup lists >= w
     uint32_t *wid = nullptr;              // [c_cap] each candidate's workgroup list
@@ -2472,7 +2475,7 @@ int zmqg_ctx_destroy(zmqg_ctx *ctx)
     {
         ZmtpWs &z = ctx->zw;
         void *zp[] = {z.F,      z.wire_off, z.cand_wg, z.count_wg, z.off_wg, z.cand, z.nb,   z.first_w,
-                      z.wid,    z.run,      z.runpre,  z.sid_fill, z.fflags, z.walk, z.temp};
+                      z.wid,    z.run,      z.runpre,  z.sid_fill, z.fflags, z.walk, z.temp, z.count16, z.cdesc, z.cflag};
         for (void *p : zp)
             if (p)
                 (void) hipFree(p);
@@ -3394,7 +3397,8 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         while (cap < nwg)
             cap *= 2;
         if ((rc = grow(ctx, z.cand_wg, cap * kZmtpWgCap, st)) || (rc = grow(ctx, z.count_wg, cap + 1, st)) ||
-            (rc = grow(ctx, z.off_wg, cap + 1, st)) || (rc = grow(ctx, z.first_w, cap + 1, st)))
+            (rc = grow(ctx, z.off_wg, cap + 1, st)) || (rc = grow(ctx, z.first_w, cap + 1, st)) ||
+            (rc = grow(ctx, z.count16, cap + 8, st)))
             return rc;
         z.g_cap = cap;
     }
@@ -3404,7 +3408,8 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         uint64_t cap = z.c_cap ? z.c_cap : 1024;
         while (cap < ccap)
             cap *= 2;
-        if ((rc = grow(ctx, z.cand, cap, st)) || (rc = grow(ctx, z.nb, cap, st)) || (rc = grow(ctx, z.wid, cap, st)))
+        if ((rc = grow(ctx, z.cand, cap, st)) || (rc = grow(ctx, z.nb, cap, st)) || (rc = grow(ctx, z.wid, cap, st)) ||
+            (rc = grow(ctx, z.cdesc, cap, st)) || (rc = grow(ctx, z.cflag, cap, st)))
             return rc;
         z.c_cap = cap;
     }
@@ -3427,14 +3432,15 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
     // 1. candidates, in stream order: per-workgroup lists, their counts'
     // exclusive sum, the lists concatenated with their links
     hipLaunchKernelGGL(k_zmtp_scan, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, max_msg_size, z.cand_wg,
-                       z.count_wg);
+                       z.count_wg, z.count16);
     ZCHECK(ctx, hipGetLastError());
-    // (ZMQG_ZMTP_CUB: the large-stream form at any size, for its tests)
-    if (nwg <= 8u * kZmtpScan1 && !getenv("ZMQG_ZMTP_CUB")) {
-        hipLaunchKernelGGL(k_zmtp_exsum, dim3(1), dim3(kZmtpScan1), 0, st, (const uint64_t *) z.count_wg, nwg,
-                           z.off_wg);
-        ZCHECK(ctx, hipGetLastError());
-    } else {
+    // The lists' offsets: up to 8,192 lists (128 MiB of stream) each
+    // compaction workgroup sums the 16-bit counts before its own list (a few
+    // 16-byte loads per thread, L2-resident) -- no launch of their own; above
+    // that, one hipCUB scan of the counts.  (ZMQG_ZMTP_CUB: the large-stream
+    // form at any size, for its tests)
+    const bool inline_sum = nwg <= kZmtpInlineSumLists && !getenv("ZMQG_ZMTP_CUB");
+    if (!inline_sum) {
         size_t need = 0;
         ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, need, z.count_wg, z.off_wg, (int) (nwg + 1), st));
         if ((rc = zmtp_temp(ctx, need, st)))
@@ -3443,18 +3449,20 @@ int zmqg_decode_zmtp_async(zmqg_ctx *ctx, uint32_t sid, const uint8_t *in, uint6
         size_t tb = z.temp_bytes;
         ZCHECK(ctx, hipcub::DeviceScan::ExclusiveSum(z.temp, tb, z.count_wg, z.off_wg, (int) (nwg + 1), st));
     }
-    hipLaunchKernelGGL(k_zmtp_compact, dim3(g), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand_wg,
-                       (const uint64_t *) z.count_wg, (const uint64_t *) z.off_wg, g, z.cand,
-                       z.nb, z.first_w, z.wid);
+    hipLaunchKernelGGL(k_zmtp_compact, dim3((g + kZmtpCompactLists - 1) / kZmtpCompactLists), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand_wg,
+                       (const uint64_t *) z.count_wg, inline_sum ? (const uint16_t *) z.count16 : nullptr, z.off_wg,
+                       g, z.cand, z.cdesc, z.cflag, z.nb, z.first_w, z.wid);
     ZCHECK(ctx, hipGetLastError());
     // 2. the first unlinked candidate after each list, then the walk (one launch)
     hipLaunchKernelGGL(k_zmtp_next_walk, dim3(1), dim3(kZmtpNextThreads), 0, st, in, in_bytes, max_msg_size,
-                       max_frames, (const uint64_t *) z.cand, m_p, (const uint64_t *) z.nb, z.first_w,
+                       max_frames, (const uint64_t *) z.cand, (const uint64_t *) z.cdesc, m_p,
+                       (const uint64_t *) z.nb, z.first_w,
                        (const uint32_t *) z.wid, nwg, z.run, z.runpre, z.walk);
     ZCHECK(ctx, hipGetLastError());
     // 3. descriptors (empty frames up to max_frames); each payload goes to
     // its body's offset in `out`, so no offsets scan is needed
-    hipLaunchKernelGGL(k_zmtp_frames, dim3(pg), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cand, m_p,
+    hipLaunchKernelGGL(k_zmtp_frames, dim3(pg), dim3(kZmtpThreads), 0, st, in, in_bytes, (const uint64_t *) z.cdesc,
+                       (const uint8_t *) z.cflag, m_p,
                        (const uint64_t *) z.run, (const uint64_t *) z.runpre, (const ZmtpWalk *) z.walk, max_frames,
                        frame_in_off, frame_len, z.fflags, z.sid_fill, sid, out_off,
                        (unsigned long long *) ((char *) z.walk + offsetof(ZmtpWalk, out_bytes)));

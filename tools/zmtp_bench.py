@@ -115,6 +115,29 @@ def main():
     assert int((st != 0).sum()) == 0 and torch.equal(zback[idx].reshape(-1), pay)
     print(f"decode_zmtp_maxmsgsize {tzm:8.1f} us  (max_msg_size = {W})")
 
+    # the same call through the C ABI alone: arguments built once, the
+    # library's own stream synchronisation the only wait (the Python
+    # wrapper's argument conversion and the extra device synchronisation
+    # above are not part of the call)
+    lib = C._lib
+    r = C.ZmtpResult()
+    args = (d._ctx, 0, C._ptr(framed), total, W, n, C._ptr(d_foff), C._ptr(d_flen), C._ptr(d_poff), C._ptr(zback),
+            C._ptr(fl), C._ptr(st), C.ctypes.byref(r), C._stream_handle(None))
+
+    def d_abi():
+        d.set_peer_nonce(0, 2)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rc = lib.zmqg_decode_zmtp(*args)
+        dt = time.perf_counter() - t0
+        assert rc == 0 and r.frames == n and r.consumed == total and r.error == 0
+        return dt
+
+    d_abi()
+    ta = sorted(d_abi() for _ in range(20))
+    assert int((st != 0).sum()) == 0
+    print(f"decode_zmtp_abi {ta[0] * 1e6:8.1f} us min, {ta[10] * 1e6:8.1f} us median  (C call, max_msg_size = {W})")
+
 
 if __name__ == "__main__":
     main()
