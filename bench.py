@@ -624,13 +624,14 @@ def config_inputs(C, torch, dev, local, rank, w, world=1):
     g.manual_seed(0xC0 + 7 * rank + int(w))
     enc, dec = C.CurveContext(local, S), C.CurveContext(local, S)
     rng = np.random.default_rng(0xC0 + rank)
-    keys = []
-    for s in range(S):
-        k = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
-        keys.append(k)
-        enc.session_set(s, k, C.CLIENT_PREFIX, C.SERVER_PREFIX)
-        enc.set_nonce(s, 3)
-        dec.session_set(s, k, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+    keys = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(S)]
+    # one install launch per context (zmqg_session_set_batch_ex): the client
+    # side continues from nonce 3 after HELLO and INITIATE, the server expects
+    # peer nonces above 2
+    precom = torch.from_numpy(np.frombuffer(b"".join(keys), np.uint8).copy()).to(dev)
+    enc.session_set_batch(np.arange(S), precom, C.CLIENT_PREFIX, C.SERVER_PREFIX, send_nonce=np.full(S, 3))
+    dec.session_set_batch(np.arange(S), precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, peer_nonce=np.full(S, 2))
+    torch.cuda.current_stream(dev).synchronize()
     t = lambda a, d: torch.from_numpy(np.ascontiguousarray(a).view(d)).to(dev)
     in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
     W = sizes + 33

@@ -126,6 +126,15 @@ int zmqg_session_set(zmqg_ctx *ctx, uint32_t sid, const uint8_t precom[32], cons
 int zmqg_session_set_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint8_t *precom,
                            const uint8_t enc_prefix[16], const uint8_t dec_prefix[16], const uint8_t *downgrade,
                            const uint64_t *peer_nonce, void *stream);
+/* The same with each session's send nonce: send_nonce is a host array of n
+ * initial send nonces, or NULL (all 1).  A connection installed after its
+ * handshake continues from the handshake's nonces -- the client's MESSAGE
+ * nonces start at 3 after HELLO (1) and INITIATE (2), src/curve_client.cpp
+ * and curve_client_tools.hpp; the server's at 2 after READY (1) -- so a
+ * mass install needs no zmqg_session_set_nonce call per session. */
+int zmqg_session_set_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint8_t *precom,
+                              const uint8_t enc_prefix[16], const uint8_t dec_prefix[16], const uint8_t *downgrade,
+                              const uint64_t *peer_nonce, const uint64_t *send_nonce, void *stream);
 
 /* curve_encoding_t::set_peer_nonce / read back _cn_peer_nonce.  Synchronous:
  * they are ordered after the work previously issued on the stream of the

@@ -394,7 +394,8 @@ __global__ void k_session_setup(DevSession *tab, unsigned long long *peer, unsig
 
 // zmqg_session_set_batch: one thread per session, the two HSalsa20 subkeys
 // of k_session_setup.  `d` (device-mapped host memory): sid[n], then
-// peer_nonce[n] (u64), then downgrade[n] (u8); precom n x 32 bytes
+// peer_nonce[n] (u64), then send_nonce[n] (u64), then downgrade[n] (u8);
+// precom n x 32 bytes
 // (device-accessible, 4-byte aligned); pfx = enc_prefix[4] dec_prefix[4].
 struct Prefixes {
     uint32_t w[8];
@@ -409,7 +410,8 @@ __global__ __launch_bounds__(256) void k_session_setup_batch(uint32_t n, const u
         return;
     const uint32_t *sid = (const uint32_t *) d;
     const unsigned long long *pn = (const unsigned long long *) (d + ((4ull * n + 7) & ~7ull));
-    const uint8_t *down = d + ((4ull * n + 7) & ~7ull) + 8ull * n;
+    const unsigned long long *sn = pn + n;
+    const uint8_t *down = d + ((4ull * n + 7) & ~7ull) + 16ull * n;
     const uint32_t s = sid[i];
     uint32_t k[8];
 #pragma unroll
@@ -424,7 +426,7 @@ __global__ __launch_bounds__(256) void k_session_setup_batch(uint32_t n, const u
         x.pad[t] = 0;
     tab[s] = x;
     peer[s] = pn[i];
-    send[s] = 1; // _cn_nonce (1), src/curve_mechanism_base.cpp:59
+    send[s] = sn[i]; // (1 unless given: _cn_nonce (1), src/curve_mechanism_base.cpp:59)
 }
 
 __global__ void k_fill_u64(unsigned long long *p, uint32_t n, unsigned long long v)
@@ -2610,6 +2612,14 @@ int zmqg_session_set_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const
                            const uint8_t enc_prefix[16], const uint8_t dec_prefix[16], const uint8_t *downgrade,
                            const uint64_t *peer_nonce, void *stream)
 {
+    return zmqg_session_set_batch_ex(ctx, n, sid, precom, enc_prefix, dec_prefix, downgrade, peer_nonce, nullptr,
+                                     stream);
+}
+
+int zmqg_session_set_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint8_t *precom,
+                              const uint8_t enc_prefix[16], const uint8_t dec_prefix[16], const uint8_t *downgrade,
+                              const uint64_t *peer_nonce, const uint64_t *send_nonce, void *stream)
+{
     if (!ctx || check_n(n))
         return -EINVAL;
     if (n == 0)
@@ -2626,7 +2636,8 @@ int zmqg_session_set_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const
         }
     }
     ZCHECK(ctx, hipSetDevice(ctx->device));
-    const size_t o_peer = (4 * n + 7) & ~(size_t) 7, o_down = o_peer + 8 * n, need = o_down + n;
+    const size_t o_peer = (4 * n + 7) & ~(size_t) 7, o_send = o_peer + 8 * n, o_down = o_send + 8 * n,
+                 need = o_down + n;
     if (ctx->sinst_done)
         ZCHECK(ctx, hipEventSynchronize(ctx->sinst_done)); // the previous install has read its descriptors
     else
@@ -2649,6 +2660,9 @@ int zmqg_session_set_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const
     uint64_t *pn = (uint64_t *) (ctx->sinst + o_peer);
     for (uint64_t i = 0; i < n; ++i)
         pn[i] = peer_nonce ? peer_nonce[i] : 1u;
+    uint64_t *sn = (uint64_t *) (ctx->sinst + o_send);
+    for (uint64_t i = 0; i < n; ++i)
+        sn[i] = send_nonce ? send_nonce[i] : 1u;
     for (uint64_t i = 0; i < n; ++i) {
         const uint8_t dg = downgrade && downgrade[i] ? 1 : 0;
         ctx->sinst[o_down + i] = dg;

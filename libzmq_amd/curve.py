@@ -55,6 +55,7 @@ _lib.zmqg_ctx_create.argtypes = [ctypes.c_int, _U32, ctypes.POINTER(_P)]
 _lib.zmqg_ctx_destroy.argtypes = [_P]
 _lib.zmqg_session_set.argtypes = [_P, _U32, _P, _P, _P, ctypes.c_int, _U64]
 _lib.zmqg_session_set_batch.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _P]
+_lib.zmqg_session_set_batch_ex.argtypes = [_P, _U64, _P, _P, _P, _P, _P, _P, _P, _P]
 _lib.zmqg_session_set_peer_nonce.argtypes = [_P, _U32, _U64]
 _lib.zmqg_session_get_peer_nonce.argtypes = [_P, _U32, ctypes.POINTER(_U64)]
 _lib.zmqg_session_set_nonce.argtypes = [_P, _U32, _U64]
@@ -183,10 +184,12 @@ class CurveContext:
         self._check(_lib.zmqg_session_set(self._ctx, sid, precom, enc_prefix, dec_prefix, int(bool(downgrade_sub)),
                                           peer_nonce), "zmqg_session_set")
 
-    def session_set_batch(self, sid, precom, enc_prefix, dec_prefix, downgrade=None, peer_nonce=None, stream=None):
-        """zmqg_session_set_batch: sid / downgrade / peer_nonce are host
-        sequences (numpy-convertible), precom a device tensor of n x 32 bytes
-        (e.g. box_beforenm_batch's k_out); asynchronous on `stream`."""
+    def session_set_batch(self, sid, precom, enc_prefix, dec_prefix, downgrade=None, peer_nonce=None, stream=None,
+                          send_nonce=None):
+        """zmqg_session_set_batch(_ex): sid / downgrade / peer_nonce /
+        send_nonce are host sequences (numpy-convertible), precom a device
+        tensor of n x 32 bytes (e.g. box_beforenm_batch's k_out); asynchronous
+        on `stream`."""
         sid = np.ascontiguousarray(sid, dtype=np.uint32)
         n = len(sid)
         enc_prefix, dec_prefix = bytes(enc_prefix), bytes(dec_prefix)
@@ -194,12 +197,14 @@ class CurveContext:
             raise ValueError("prefixes must be 16 bytes")
         dg = None if downgrade is None else np.ascontiguousarray(downgrade, dtype=np.uint8)
         pn = None if peer_nonce is None else np.ascontiguousarray(peer_nonce, dtype=np.uint64)
-        if (dg is not None and len(dg) != n) or (pn is not None and len(pn) != n):
-            raise ValueError("downgrade / peer_nonce must have one entry per session")
-        self._check(_lib.zmqg_session_set_batch(self._ctx, n, sid.ctypes.data, _ptr(precom), enc_prefix, dec_prefix,
-                                                None if dg is None else dg.ctypes.data,
-                                                None if pn is None else pn.ctypes.data, _stream_handle(stream)),
-                    "zmqg_session_set_batch")
+        sn = None if send_nonce is None else np.ascontiguousarray(send_nonce, dtype=np.uint64)
+        if (dg is not None and len(dg) != n) or (pn is not None and len(pn) != n) or (sn is not None and len(sn) != n):
+            raise ValueError("downgrade / peer_nonce / send_nonce must have one entry per session")
+        self._check(_lib.zmqg_session_set_batch_ex(self._ctx, n, sid.ctypes.data, _ptr(precom), enc_prefix,
+                                                   dec_prefix, None if dg is None else dg.ctypes.data,
+                                                   None if pn is None else pn.ctypes.data,
+                                                   None if sn is None else sn.ctypes.data, _stream_handle(stream)),
+                    "zmqg_session_set_batch_ex")
         for i, s in enumerate(sid.tolist()):
             self.downgrade[s] = bool(dg[i]) if dg is not None else False
 

@@ -126,3 +126,38 @@ def test_batch_install_rejects_bad_sids(torch_cuda, C):
     ctx.session_set_batch([1, 2, 3], k, C.CLIENT_PREFIX, C.SERVER_PREFIX)
     torch.cuda.synchronize()
     assert ctx.get_nonce(2) == 1 and ctx.get_peer_nonce(3) == 1
+
+
+def test_batch_install_send_nonces(torch_cuda, C):
+    """zmqg_session_set_batch_ex: each session's send nonce as installed (a
+    client connection continues from 3 after HELLO and INITIATE), and the
+    first nonce-auto encode takes it, against the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77)
+    keys = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(4)]
+    k = torch.from_numpy(np.frombuffer(b"".join(keys), np.uint8).copy()).to("cuda")
+    ctx = C.CurveContext(0, 4)
+    sn = np.array([3, 10, 1 << 33, 7], np.uint64)
+    ctx.session_set_batch([2, 0, 3, 1], k, C.CLIENT_PREFIX, C.SERVER_PREFIX, peer_nonce=[5, 6, 7, 8],
+                          send_nonce=sn)
+    torch.cuda.synchronize()
+    assert [ctx.get_nonce(s) for s in (2, 0, 3, 1)] == [int(x) for x in sn]
+    assert [ctx.get_peer_nonce(s) for s in (2, 0, 3, 1)] == [5, 6, 7, 8]
+    # one 100-byte frame per session, nonces assigned on the device
+    sid = np.array([0, 1, 2, 3], np.uint32)
+    lens = np.full(4, 100, np.uint32)
+    flags = np.zeros(4, np.uint8)
+    payloads = [rng.integers(0, 256, 100, dtype=np.uint8).tobytes() for _ in range(4)]
+    inp, in_off = pack(payloads, rng, 3)
+    w_off, w_len, w_total = wire_layout(flags, lens, np.zeros(4, np.uint8), sid, rng, 3)
+    wire = torch.zeros(w_total, dtype=torch.uint8, device="cuda")
+    ctx.encode_batch(_dev(torch, sid), None, _dev(torch, flags), _dev(torch, in_off), _dev(torch, lens),
+                     _dev(torch, inp), _dev(torch, w_off), wire, nonce_auto=True)
+    torch.cuda.synchronize()
+    by_sid = {2: keys[0], 0: keys[1], 3: keys[2], 1: keys[3]}
+    nonce_by_sid = {2: 3, 0: 10, 3: 1 << 33, 1: 7}
+    osess = _oracle_sessions([by_sid[s] for s in range(4)], O.CLIENT_PREFIX, O.SERVER_PREFIX, np.zeros(4, np.uint8))
+    nonce = np.array([nonce_by_sid[int(s)] for s in sid], np.uint64)
+    want = O.encode_batch(osess, sid, nonce, flags, in_off, lens, inp, w_off, w_total)
+    assert np.array_equal(wire.cpu().numpy(), want)
+    assert [ctx.get_nonce(s) for s in (2, 0, 3, 1)] == [int(x) + 1 for x in sn]
