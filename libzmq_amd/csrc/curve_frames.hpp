@@ -57,6 +57,9 @@ __device__ __forceinline__ void seq_store4(uint64_t a, uint32_t x, uint32_t y, u
         *(G4_ *) (uintptr_t) a = (v4_){x, y, z, w};
 }
 
+#ifndef ZMQG_SEQ_LDSIN
+#define ZMQG_SEQ_LDSIN 1 // k_frames_seq: each window's input staged by the wave's LDS-DMA one window ahead (1; 0: per-lane loads)
+#endif
 #ifndef ZMQG_SEQ_PF
 #define ZMQG_SEQ_PF 1 // k_frames_seq: windows requested ahead of the one computed (1; 2 measured slower)
 #endif
@@ -1177,6 +1180,35 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 //   * Decode reads window 0 (header, nonce, tag, first ciphertext) in one
 //     load with the header checks taken from it; encode fetches the payload's
 //     first bytes with the descriptors.
+// ---- LDS-DMA staging, shared by k_frames_lds and k_frames_seq's staged input
+constexpr uint32_t kStIn = 80; // input slot: a 64-byte window's 16-byte-aligned cover (5 granules)
+typedef u32x4 u32x4_u1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) void StLdsVoid;
+
+// One LDS-DMA granule per lane: global [gaddr, +16) -> LDS lds_base + 16 * lane
+// (global_load_lds_dwordx4).  Issued from inline asm so that the compiler
+// does not treat it as an LDS write of unknown extent: it would then wait for
+// it (vmcnt(0)) before every later LDS access of the wave.  The kernel orders
+// it itself: one explicit vmcnt(0) at the top of the step that reads the
+// buffer, and a buffer is only refilled a step after it was last read.
+__device__ __forceinline__ void lds_dma16(uint64_t gaddr, uint32_t lds_base)
+{
+    // M0 is the compiler's: saved and restored in the same statement
+    // (cdna_hip_programming.md section 5.7)
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gaddr), "s"(lds_base)
+                 : "memory");
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src)
+{
+    const uint32_t lo = (uint32_t) __shfl((int) (uint32_t) v, (int) src);
+    const uint32_t hi = (uint32_t) __shfl((int) (uint32_t) (v >> 32), (int) src);
+    return ((uint64_t) hi << 32) | lo;
+}
+
 // Same frame semantics, replay rule, big-frame hand-off and call state as
 // k_frames with G = 1.
 template <bool DEC, class BigOp>
@@ -1345,7 +1377,41 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     // requested two steps before it is used (inputs from HBM rather than the
     // Infinity Cache take longer than one keystream to arrive)
     uint32_t ddA[16], ddB[16];
-    bool fastA = nw > 1u ? frame_prefetch(A4, lim, wave_end, 1u, ddA) : true, fastB = true;
+    bool fastA = !ZMQG_SEQ_LDSIN && nw > 1u ? frame_prefetch(A4, lim, wave_end, 1u, ddA) : true, fastB = true;
+    // ZMQG_SEQ_LDSIN: the wave moves its 64 frames' window covers (five
+    // 16-byte granules each, the k_frames_lds input path) into one of two
+    // LDS buffers by LDS-DMA, a window ahead; pair j of lane l moves granule
+    // (64j + l) % 5 of frame (64j + l) / 5, so each instruction covers runs of
+    // whole 80-byte covers instead of 64 lanes' scattered 16-byte pieces, and
+    // the owning lane reads its window at its byte offset (unaligned
+    // ds_read_b128): no alignbyte shifts, no register buffers held across a
+    // keystream
+    __shared__ __attribute__((aligned(16))) uint8_t sq_lds[ZMQG_SEQ_LDSIN ? kFramesWaves * 2 * 64 * kStIn : 16];
+    uint8_t *const sq_w = sq_lds + (ZMQG_SEQ_LDSIN ? (threadIdx.x >> 6) * 2 * 64 * kStIn : 0u);
+    const uint32_t sq_off = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (StLdsVoid *) sq_w);
+    const uint32_t sq_va = (uint32_t) A & 15u;
+    uint64_t sq_la[5];
+    uint32_t sq_rel[5], sq_lim[5];
+    if (ZMQG_SEQ_LDSIN) {
+        const uint64_t Ab = A - sq_va;
+        const uint32_t lm = S ? sq_va + S : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) {
+            const uint32_t idx = 64u * j + lane, f = idx / 5u, k = idx - 5u * f;
+            sq_rel[j] = 16u * k;
+            sq_la[j] = shfl_u64(Ab, f) + sq_rel[j];
+            sq_lim[j] = (uint32_t) __shfl((int) lm, (int) f);
+        }
+    }
+    auto sq_dma = [&](uint32_t t) { // window t's covers -> buffer t & 1 (granules holding a stream byte)
+        const uint32_t b = sq_off + (t & 1u) * 64u * kStIn;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j)
+            if (64u * t + sq_rel[j] < sq_lim[j])
+                lds_dma16(sq_la[j] + 64ull * t, b + 1024u * j);
+    };
+    if (ZMQG_SEQ_LDSIN && steps > 1u)
+        sq_dma(1u);
 #if ZMQG_SEQ_PF == 2
     uint32_t ddC[16];
     bool fastC = true;
@@ -1511,7 +1577,22 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
         }
         SEQ_STAMP(24u + t);
         uint32_t x[16], w16; // w16: this window's word 16 = the next window's word 0
-        if (__builtin_amdgcn_ballot_w64(act && !fast) != 0) {
+        if (ZMQG_SEQ_LDSIN) {
+            // window t's covers have landed (and the stores of a step ago
+            // are out of the way)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const uint8_t *const p = sq_w + (t & 1u) * 64u * kStIn + kStIn * lane + sq_va;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const u32x4 u = *(const u32x4_u1 *) (p + 16u * q);
+                x[4 * q] = u.x;
+                x[4 * q + 1] = u.y;
+                x[4 * q + 2] = u.z;
+                x[4 * q + 3] = u.w;
+            }
+            w16 = 0;
+        } else if (__builtin_amdgcn_ballot_w64(act && !fast) != 0) {
             // a lane whose words were not prefetched (the end of the wave's
             // furthest frame) reads them exactly
             uint32_t ee[16];
@@ -1563,6 +1644,9 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
             for (int k = 0; k < 16; ++k)
                 dn[k] = y[k] + k;
             fastn = true;
+        } else if (ZMQG_SEQ_LDSIN) {
+            if (t + 1u < steps)
+                sq_dma(t + 1u);
         } else if (ZMQG_SEQ_PF == 1 && t + 1u < nw) {
             fastn = frame_prefetch(A4, lim, wave_end, t + 1u, dn);
         }

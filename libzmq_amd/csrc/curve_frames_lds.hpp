@@ -76,13 +76,10 @@ constexpr uint32_t kStSector = ZMQG_LDS_SECTOR;
 constexpr uint32_t kStNIn = ZMQG_LDS_INBUF;
 static_assert(kStSector == 16 || kStSector == 64, "output sector");
 static_assert(kStNIn == 1 || kStNIn == 2, "input buffers");
-constexpr uint32_t kStIn = 80;                                  // input slot: a window's 16-byte-aligned cover
 constexpr uint32_t kStRing = 128 + kStSector;                   // output ring slot
 constexpr uint32_t kStInBuf = 64 * kStIn;                       // one input buffer per wave
 constexpr uint32_t kStWave = kStNIn * kStInBuf + 64 * kStRing;  // 19,456 bytes per wave (16, 2)
 
-typedef u32x4 u32x4_u1 __attribute__((aligned(1)));
-typedef __attribute__((address_space(3))) void StLdsVoid;
 typedef __attribute__((address_space(1))) void StGVoid;
 
 // bytes [lo, hi) (0 <= lo < hi <= 16) of granule v at the 16-byte aligned
@@ -115,30 +112,6 @@ __device__ __forceinline__ void granule_store_part(uint64_t a, uint32_t lo, uint
     for (uint32_t b = 0; b < 3; ++b)
         if (ts + b < hi && la < 4u)
             *(GU8 *) (uintptr_t) (a + ts + b) = (uint8_t) (wt >> (8u * ((ts + b) & 3u)));
-}
-
-// One LDS-DMA granule per lane: global [gaddr, +16) -> LDS lds_base + 16 * lane
-// (global_load_lds_dwordx4).  Issued from inline asm so that the compiler
-// does not treat it as an LDS write of unknown extent: it would then wait for
-// it (vmcnt(0)) before every later LDS access of the wave.  The kernel orders
-// it itself: one explicit vmcnt(0) at the top of the step that reads the
-// buffer, and a buffer is only refilled a step after it was last read.
-__device__ __forceinline__ void lds_dma16(uint64_t gaddr, uint32_t lds_base)
-{
-    // M0 is the compiler's: saved and restored in the same statement
-    // (cdna_hip_programming.md section 5.7)
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gaddr), "s"(lds_base)
-                 : "memory");
-}
-
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src)
-{
-    const uint32_t lo = (uint32_t) __shfl((int) (uint32_t) v, (int) src);
-    const uint32_t hi = (uint32_t) __shfl((int) (uint32_t) (v >> 32), (int) src);
-    return ((uint64_t) hi << 32) | lo;
 }
 
 template <bool DEC, class BigOp>
