@@ -355,6 +355,12 @@ def main():
     if d:
         traffic = d.get("read_bytes_per_launch")
         traffic_write = d.get("write_bytes_per_launch")
+        # the HBM-fed form's own pass (tools/hbm_probe.py --forms bench, same build)
+        hd = (d.get("hbm_fed") or {}).get("decode")
+        if hbm and hd:
+            hbm["roofline"]["traffic"] = hd.get("read_bytes_per_launch")
+            hbm["roofline"]["traffic_write"] = hd.get("write_bytes_per_launch")
+            hbm["roofline"]["l2_memory_side_requests"] = hd.get("l2_memory_side_requests_per_launch")
     # The kernel is VALU-issue bound: its VALU
     # instruction count per launch (committed PMC pass) over the same live
     # launch duration, against the chip's VALU issue peak (1024 SIMDs x 16
@@ -542,7 +548,8 @@ def hbm_fed(torch, dev, stream, enc, dec, K, n, W, P, sid, flags, in_off, lens, 
         ev[1].record(stream)
         ev[2].record(stream)
         for k in range(K):
-            dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream, max_len=W)
+            dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream, max_len=W,
+                             stream_out=True)
         ev[3].record(stream)
         torch.cuda.synchronize(dev)
         return ev[0].elapsed_time(ev[1]) / 1e3, ev[2].elapsed_time(ev[3]) / 1e3
@@ -562,7 +569,8 @@ def hbm_fed(torch, dev, stream, enc, dec, K, n, W, P, sid, flags, in_off, lens, 
            "sets": K, "bytes_per_set": n * (2 * P + W),
            "note": f"{K} config-2 batches with their own buffers ({K * n * (2 * P + W) / 2**20:.0f} MiB against "
                    f"the 256 MiB Infinity Cache): {K} encodes back to back, then their {K} decodes, one event pair "
-                   "each; every input comes from HBM"}
+                   "each; every input comes from HBM; the decodes pass ZMQG_OPT_STREAM_OUT, the cache hint for "
+                   "outputs no cache holds (whole-segment stores)"}
     del pays, wires, backs
     torch.cuda.empty_cache()
     return out

@@ -261,11 +261,23 @@ int zmqg_decode_batch(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const uint
  *                    per frame 0 (open it) or the ZMQG_ERR_* code the host's
  *                    rules gave it, which is then the frame's status (its
  *                    payload region zero-filled, flags 0).
+ *   flags            ZMQG_OPT_STREAM_OUT (decode): a cache hint, results
+ *                    unchanged.  The decoded payloads go to memory the
+ *                    device's caches do not hold (batches rotating over more
+ *                    buffers than the 256 MiB Infinity Cache keeps, as a
+ *                    receive ring does): each 64-byte payload piece leaves as
+ *                    a whole segment, a wave's 16 frames per store, staged
+ *                    through LDS, instead of each lane's own 16-byte pieces.
+ *                    Config 2 from HBM: 60 against 75 us per decode; with the
+ *                    output lines already cached it costs ~5 us
+ *                    (DESIGN.md section 3.1).  Applies to the one-lane-per-
+ *                    frame kernel when every payload starts 64-byte aligned.
  * A caller built against the struct without out_bytes (or verdict_in)
  * passes the smaller size and gets the old behaviour. */
 #define ZMQG_OPT_NONCE_AUTO 1u
 #define ZMQG_OPT_VERIFY_FIRST 2u
 #define ZMQG_OPT_REPLAY_HOST 4u
+#define ZMQG_OPT_STREAM_OUT 8u
 typedef struct zmqg_batch_opts {
     uint32_t size;
     uint32_t flags;

@@ -60,6 +60,9 @@ __device__ __forceinline__ void seq_store4(uint64_t a, uint32_t x, uint32_t y, u
 #ifndef ZMQG_SEQ_LDSIN
 #define ZMQG_SEQ_LDSIN 1 // k_frames_seq: each window's input staged by the wave's LDS-DMA one window ahead (1; 0: per-lane loads)
 #endif
+#ifndef ZMQG_SEQ_COOPST
+#define ZMQG_SEQ_COOPST 2 // k_frames_seq decode under ZMQG_OPT_STREAM_OUT, 64-byte-aligned payloads: each step's chunks stored by the wave cooperatively (16 frames x 64 B per instruction) through LDS, a step later (2; 3: at the next step's top) or at once (1); 0: each lane its own always
+#endif
 #ifndef ZMQG_SEQ_PF
 #define ZMQG_SEQ_PF 1 // k_frames_seq: windows requested ahead of the one computed (1; 2 measured slower)
 #endif
@@ -363,6 +366,7 @@ struct FrameCtl {
     // on frames [0, split_n) (split_n = split_wg x kFramesBS), the rest run the
     // G-lanes-per-frame body on frames [split_n, n); 0 in every other launch
     uint32_t split_wg, split_n;
+    uint32_t stream_out; // decode, ZMQG_OPT_STREAM_OUT (host side: picks k_frames_seq's SO instantiation)
 };
 
 // msg_t flags a received ZMTP frame adds to its decoded message: the
@@ -1211,7 +1215,7 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src)
 
 // Same frame semantics, replay rule, big-frame hand-off and call state as
 // k_frames with G = 1.
-template <bool DEC, class BigOp>
+template <bool DEC, class BigOp, bool SO = false>
 #ifndef ZMQG_SEQ_WPE
 #define ZMQG_SEQ_WPE 0 // k_frames_seq: minimum waves per SIMD the register allocation must allow (0: no bound)
 #endif
@@ -1429,6 +1433,33 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     // per window.
     const bool al64 = ZMQG_SEQ_AL64 && DEC && __builtin_amdgcn_ballot_w64(((uint32_t) (uintptr_t) dst & 63u) != 0u) == 0;
     uint32_t yp[16]; // al64: the previous window's output words
+    // ZMQG_SEQ_COOPST (al64 decode): each lane puts its 64-byte chunk into the
+    // wave's LDS staging area, and store j of lane l writes 16 bytes (l % 4)
+    // of frame 16j + l / 4's chunk -- each instruction whole 64-byte segments
+    // of 16 frames instead of 16-byte pieces of 64 frames' segments, which
+    // the L2 wrote back as partial segments (WRITE_SIZE 1.41x the payload,
+    // TCC_EA0_WRREQ_64B 1.49 M requests per launch for 1.05 M segments;
+    // profiles/pmc_traffic_config2.json)
+    // ZMQG_SEQ_COOPST 2: a step's chunks go into the staging area at its end
+    // and leave in the next step -- read back at its top, stored after its
+    // keystream -- so the single wave on the SIMD never waits on the LDS
+    // round trip (form 1, read back and stored at once, costs the resident
+    // decode ~8 us per launch)
+    bool cs_pend = false; // the staging area holds the previous step's chunks
+    __shared__ __attribute__((aligned(16))) uint8_t sq_stg[ZMQG_SEQ_COOPST && SO ? kFramesWaves * 64 * 64 : 16];
+    uint8_t *const stg = sq_stg + (ZMQG_SEQ_COOPST && SO ? (threadIdx.x >> 6) * 64u * 64u : 0u);
+    uint64_t cs_dst[4];
+    uint32_t cs_nw[4];
+    // (SO: the ZMQG_OPT_STREAM_OUT instantiation; al64 is wave-uniform)
+    const bool coop = ZMQG_SEQ_COOPST && SO && DEC && al64;
+    if (coop) {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t f = 16u * j + (lane >> 2);
+            cs_dst[j] = shfl_u64((uint64_t) (uintptr_t) dst, f) + 16u * (lane & 3u);
+            cs_nw[j] = (uint32_t) __shfl((int) nw, (int) f);
+        }
+    }
     uint32_t ct0[8]; // encode: window 0's ciphertext words (stored with the tag)
 
     SEQ_STAMP(1u);
@@ -1532,6 +1563,23 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     auto step = [&](uint32_t t, uint32_t (&dd)[16], bool &fast, uint32_t (&dn)[16], bool &fastn) {
         SEQ_STAMP(3u + t);
         const bool act = t < nw;
+        // (COOPST 2) the previous step's staged chunks, read now, stored
+        // after the keystream
+        const bool had = ZMQG_SEQ_COOPST >= 2 && coop && cs_pend;
+        u32x4 cg[4];
+        if (had) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                cg[j] = *(const u32x4 *) (stg + 64u * (16u * j + (lane >> 2)) + 16u * (lane & 3u));
+            if (ZMQG_SEQ_COOPST == 3) { // stored here, a whole keystream ahead of the next step's wait
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (t - 1u < cs_nw[j])
+                        seq_store4(cs_dst[j] + 64ull * (t - 2u), cg[j].x, cg[j].y, cg[j].z, cg[j].w);
+                cs_pend = false;
+            }
+        }
 #if ZMQG_SEQ_PF == 2
         // window t+2 into the buffer window t-1 has left
         if (t + 2u < nw)
@@ -1668,7 +1716,38 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
                 o[k] = __builtin_amdgcn_alignbyte(y[k - 7], y[k - 8], 1);
             uint8_t *const cdst = dst + 64u * (t - 1u);
             const bool lastw = act && t + 1u == nw;
-            if (__builtin_amdgcn_ballot_w64(lastw) == 0) {
+            if (ZMQG_SEQ_COOPST == 2 && had) { // chunk t-2 of every frame that was active a step ago
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (t - 1u < cs_nw[j])
+                        seq_store4(cs_dst[j] + 64ull * (t - 2u), cg[j].x, cg[j].y, cg[j].z, cg[j].w);
+                cs_pend = false;
+            }
+            if (ZMQG_SEQ_COOPST >= 2 && coop && __builtin_amdgcn_ballot_w64(lastw) == 0) {
+                // (no lane on its last window: every active frame's chunk is
+                // whole; a later step is certain -- the wave's longest frame
+                // has not reached its last window -- and stores them)
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // (after this step's reads)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *(u32x4 *) (stg + 64u * lane + 16u * k) = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                cs_pend = true;
+            } else if (ZMQG_SEQ_COOPST == 1 && coop && __builtin_amdgcn_ballot_w64(lastw) == 0) {
+                // (no lane on its last window: every active frame's chunk is whole)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *(u32x4 *) (stg + 64u * lane + 16u * k) = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                u32x4 g[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    g[j] = *(const u32x4 *) (stg + 64u * (16u * j + (lane >> 2)) + 16u * (lane & 3u));
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (t < cs_nw[j])
+                        seq_store4(cs_dst[j] + 64ull * (t - 1u), g[j].x, g[j].y, g[j].z, g[j].w);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // (the reads before the next step's writes)
+            } else if (__builtin_amdgcn_ballot_w64(lastw) == 0) {
                 if (act) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
@@ -1816,10 +1895,10 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     }
 }
 
-template <bool DEC, class BigOp>
+template <bool DEC, class BigOp, bool SO = false>
 __global__ __launch_bounds__(kFramesBS) ZMQG_SEQ_ATTR void k_frames_seq(ZMQG_FRAMES_PARAMS)
 {
-    frames_seq_impl<DEC, BigOp>(ZMQG_FRAMES_ARGS);
+    frames_seq_impl<DEC, BigOp, SO>(ZMQG_FRAMES_ARGS);
 }
 
 // Batches just above one wave per SIMD (slots < n <= 3 slots / 2): the

@@ -232,8 +232,8 @@ struct zmqg_ctx {
     std::vector<uint8_t> h_downgrade; // host copy of each session's downgrade_sub
     // profiling: event pairs per kind, recycled through a pool
     bool profiling = false;
-    int frames_cap[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1, 2, 4,
-                                                  // seq, lds, split 2, 4, 8
+    int frames_cap[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; // decode frame-kernel workgroups resident at once, G = 1,
+                                                     // 2, 4, seq, lds, split 2, 4, 8, seq under STREAM_OUT
     int force_g = -1;                 // ZMQG_FRAMES_G: frame-kernel variant override (experiments)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[6];
     std::vector<hipEvent_t> event_pool;
@@ -2202,9 +2202,9 @@ static uint64_t frames_grid(const zmqg_ctx *ctx, int G, uint32_t n)
 // Workgroups of the decode frame kernel the device holds at once (occupancy
 // query x CUs; the kernel is VGPR-limited, where the query is exact --
 // MI355X_MICROARCH.md, Residency), cached per variant.
-int frames_capacity(zmqg_ctx *ctx, int G)
+int frames_capacity(zmqg_ctx *ctx, int G, bool so = false)
 {
-    int &c = ctx->frames_cap[G == 24 ? 7 : G == 20 ? 6 : G == 18 ? 5 : G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0
+    int &c = ctx->frames_cap[G == 0 && so ? 8 : G == 24 ? 7 : G == 20 ? 6 : G == 18 ? 5 : G == 8 ? 4 : G == 0 ? 3 : G == 1 ? 0
                              : G == 2 ? 1 : 2];
     if (c == 0) {
         int nb = 0;
@@ -2213,6 +2213,7 @@ int frames_capacity(zmqg_ctx *ctx, int G)
             : G == 20 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_split<true, 4, DecodeHead>, kFramesBS, 0)
             : G == 18 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_split<true, 2, DecodeHead>, kFramesBS, 0)
             : G == 8  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_lds<true, DecodeHead>, kFramesBS, 0)
+            : G == 0 && so ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead, true>, kFramesBS, 0)
             : G == 0  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames_seq<true, DecodeHead>, kFramesBS, 0)
             : G == 1  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 1, DecodeHead>, kFramesBS, 0)
             : G == 2  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_frames<true, 2, DecodeHead>, kFramesBS, 0)
@@ -2254,6 +2255,14 @@ void launch_frames(const zmqg_ctx *ctx, int G, uint32_t n, hipStream_t st, const
         return;
     }
     if (G == 0) {
+        if constexpr (DEC) {
+            if (ctl.stream_out) { // ZMQG_OPT_STREAM_OUT: whole-segment output stores
+                hipLaunchKernelGGL((k_frames_seq<DEC, BigOp, true>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags,
+                                   in_off, len, in, out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out,
+                                   status_out, rp, big, zs, ctl);
+                return;
+            }
+        }
         hipLaunchKernelGGL((k_frames_seq<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
                            out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
                            ctl);
@@ -2937,6 +2946,7 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
     if (opts) {
         ctl.max_len = opts->max_len;
         ctl.no_body = opts->max_len && opts->max_len <= kMaxFrameStream;
+        ctl.stream_out = (opts->flags & ZMQG_OPT_STREAM_OUT) ? 1u : 0u;
         smax = (unsigned long long *) opts->session_max_out;
     }
     if (verify_first) { // frames whose payload would leave the staging area fail with ZMQG_ERR_BOUND
@@ -2974,9 +2984,9 @@ static int decode_batch_impl(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, con
         // whatever the dispatch order); a larger one takes tickets.
         // (a split launch needs that order: its two bodies are told apart by
         // blockIdx; without it the batch runs one lane per frame)
-        if (G >= 16 && frames_grid(ctx, G, nn) > (uint64_t) frames_capacity(ctx, G))
+        if (G >= 16 && frames_grid(ctx, G, nn) > (uint64_t) frames_capacity(ctx, G, ctl.stream_out))
             G = 0;
-        rp.ordered = frames_grid(ctx, G, nn) <= (uint64_t) frames_capacity(ctx, G) ? 1u : 0u;
+        rp.ordered = frames_grid(ctx, G, nn) <= (uint64_t) frames_capacity(ctx, G, ctl.stream_out) ? 1u : 0u;
     }
     ProfSpan call(ctx, ZMQG_PROF_DECODE_CALL, st);
     ProfSpan main(ctx, ZMQG_PROF_DECODE_MAIN, st);

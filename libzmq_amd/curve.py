@@ -67,6 +67,7 @@ _lib.zmqg_decode_batch.argtypes = [_P, _U64] + [_P] * 9
 OPT_NONCE_AUTO = 1  # zmqg_batch_opts.flags: encode nonces from the sessions' send counters
 OPT_VERIFY_FIRST = 2  # zmqg_batch_opts.flags: decode writes out only after each frame's verdict
 OPT_REPLAY_HOST = 4  # zmqg_batch_opts.flags: the caller applied the header / replay rules (verdict_in)
+OPT_STREAM_OUT = 8  # zmqg_batch_opts.flags: decode output not cache-resident (whole-segment stores; a hint)
 
 
 class BatchOpts(ctypes.Structure):  # zmqg_batch_opts
@@ -247,12 +248,12 @@ class CurveContext:
     # nonce_auto: encode takes nonces from the sessions' send counters (nonce may be None)
     @staticmethod
     def _opts(max_len, status_out, session_max_out, nonce_auto=False, verify_first=False, out_bytes=0,
-              verdict_in=None):
+              verdict_in=None, stream_out=False):
         if (not max_len and status_out is None and session_max_out is None and not nonce_auto and not verify_first
-                and verdict_in is None):
+                and verdict_in is None and not stream_out):
             return None
         fl = ((OPT_NONCE_AUTO if nonce_auto else 0) | (OPT_VERIFY_FIRST if verify_first else 0)
-              | (OPT_REPLAY_HOST if verdict_in is not None else 0))
+              | (OPT_REPLAY_HOST if verdict_in is not None else 0) | (OPT_STREAM_OUT if stream_out else 0))
         o = BatchOpts(ctypes.sizeof(BatchOpts), fl, int(max_len or 0), _ptr(status_out), _ptr(session_max_out),
                       int(out_bytes), _ptr(verdict_in))
         return ctypes.byref(o), o
@@ -266,18 +267,20 @@ class CurveContext:
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_encode_batch")
 
     def decode_batch(self, sid, in_off, wire_len, inp, out_off, out, flags_out, status_out, stream=None, max_len=0,
-                     session_max_out=None, verify_first=False, out_bytes=None, verdict_in=None):
+                     session_max_out=None, verify_first=False, out_bytes=None, verdict_in=None, stream_out=False):
         """session_max_out: int64 tensor of max_sessions entries (device),
         receives each session's largest header-valid nonce of the batch.
         verify_first: ZMQG_OPT_VERIFY_FIRST (out receives only verified
         payloads and zeros; out's extent is taken from the tensor unless
         out_bytes is given).  verdict_in: int32 tensor (device) of the host's
-        header / replay verdicts, ZMQG_OPT_REPLAY_HOST (with verify_first)."""
+        header / replay verdicts, ZMQG_OPT_REPLAY_HOST (with verify_first).
+        stream_out: ZMQG_OPT_STREAM_OUT, the cache hint for outputs the device's
+        caches do not hold."""
         n = int(sid.numel())
         if out_bytes is None:
             out_bytes = out.numel() * out.element_size() if verify_first else 0
         o = self._opts(max_len, None, session_max_out, verify_first=verify_first, out_bytes=out_bytes,
-                       verdict_in=verdict_in)
+                       verdict_in=verdict_in, stream_out=stream_out)
         self._check(_lib.zmqg_decode_batch_ex(self._ctx, n, _ptr(sid), _ptr(in_off), _ptr(wire_len), _ptr(inp),
                                               _ptr(out_off), _ptr(out), _ptr(flags_out), _ptr(status_out),
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_decode_batch")

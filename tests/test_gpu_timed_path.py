@@ -12,7 +12,11 @@ of the send-nonce pre-pass over many tiles.
   replay rule (src/curve_mechanism_base.cpp:98-106, the peer nonce advanced
   before the MAC check) against the oracle's sequential decode.
 * NONCE_AUTO over several sessions above 262,144 frames, where the nonce
-  pre-pass scans its tile table in two or more row blocks."""
+  pre-pass scans its tile table in two or more row blocks.
+* ZMQG_OPT_STREAM_OUT (decode, a cache hint: whole-segment output stores
+  staged through LDS) on the replay batch and on mixed lengths whose payloads
+  start 64-byte aligned, so lanes reach their last window at different
+  steps -- the same bytes, statuses and flags as the oracle."""
 import os
 
 import numpy as np
@@ -79,8 +83,9 @@ def test_bench_step_bitexact(torch_cuda, C, variant):
         assert dec.get_peer_nonce(0) == 2 + (step + 1) * N
 
 
+@pytest.mark.parametrize("stream_out", [False, True])
 @pytest.mark.parametrize("variant", VARIANTS)
-def test_one_session_decode_replays_across_workgroups(torch_cuda, C, variant):
+def test_one_session_decode_replays_across_workgroups(torch_cuda, C, variant, stream_out):
     torch = torch_cuda
     rng = np.random.default_rng(78)
     precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
@@ -110,7 +115,7 @@ def test_one_session_decode_replays_across_workgroups(torch_cuda, C, variant):
     fl = torch.zeros(N, dtype=torch.uint8, device="cuda")
     st = torch.zeros(N, dtype=torch.int32, device="cuda")
     dec.decode_batch(dev(torch, sid), dev(torch, out_off), dev(torch, np.full(N, W, np.uint32)), dev(torch, wire),
-                     dev(torch, in_off), back, fl, st, max_len=W)
+                     dev(torch, in_off), back, fl, st, max_len=W, stream_out=stream_out)
     torch.cuda.synchronize()
     gst = host(st, np.int32)
     assert np.array_equal(gst, rst[:N]), np.nonzero(gst != rst[:N])[0][:10]
@@ -163,3 +168,55 @@ def test_nonce_auto_many_tiles_several_sessions(torch_cuda, C):
         ref = O.encode_batch(sess, sid[pick], got[pick], flags[pick], in_off[pick], np.full(pick.size, L, np.uint32),
                              inp, np.arange(pick.size, dtype=np.uint64) * Wn, pick.size * Wn)
         assert np.array_equal(ref.reshape(pick.size, Wn), w[pick])
+
+
+@pytest.mark.parametrize("variant", ["default", "0"])
+def test_stream_out_mixed_lengths(torch_cuda, C, variant):
+    """ZMQG_OPT_STREAM_OUT over payloads of 0 ... 4,400 bytes at 64-byte
+    aligned offsets (the staged whole-segment stores apply), packed wire,
+    one session with a replay and a tampered frame: lanes reach their last
+    window at different steps, so staged chunks and each lane's own tail
+    stores interleave -- against the oracle's sequential decode."""
+    torch = torch_cuda
+    rng = np.random.default_rng(80)
+    n = 20000
+    lens = rng.integers(0, 4400, n).astype(np.uint32)
+    lens[::97] = 0
+    lens[5::101] = 64 * rng.integers(1, 60, lens[5::101].size)
+    slot = (lens.astype(np.uint64) + 63) // 64 * 64 + 64 * rng.integers(0, 2, n).astype(np.uint64)
+    in_off = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64)
+    W_ = lens.astype(np.uint64) + 33
+    out_off = np.concatenate([[0], np.cumsum(W_)[:-1]]).astype(np.uint64)
+    precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    sid = np.zeros(n, np.uint32)
+    nonce = np.arange(3, 3 + n, dtype=np.uint64)
+    nonce[9000] = nonce[8000]  # replay across workgroups
+    flags = (rng.integers(0, 4, n) == 0).astype(np.uint8)
+    total = int(in_off[-1] + slot[-1])
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    sess = O.make_sessions([precom])
+    wtot = int(out_off[-1] + W_[-1])
+    wire = O.encode_batch(sess, sid, nonce, flags, in_off, lens, inp, out_off, wtot)
+    big = int(np.nonzero(lens > 2000)[0][3])
+    wire[out_off[big] + 1500] ^= 0x04  # MAC failure
+    dsess = O.make_sessions([precom], enc_prefix=O.SERVER_PREFIX, dec_prefix=O.CLIENT_PREFIX)
+    peer = np.array([2], np.uint64)
+    rpl, rfl, rst = O.decode_batch(dsess, peer, sid, out_off, W_.astype(np.uint32), wire, in_off, total)
+    assert rst[9000] != 0 and rst[big] != 0
+    dec = _ctx(C, variant)
+    dec.session_set(0, precom, O.SERVER_PREFIX, O.CLIENT_PREFIX, False, 2)
+    back = torch.full((total,), 0xEE, dtype=torch.uint8, device="cuda")
+    fl = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    dec.decode_batch(dev(torch, sid), dev(torch, out_off), dev(torch, W_.astype(np.uint32)), dev(torch, wire),
+                     dev(torch, in_off), back, fl, st, max_len=int(W_.max()), stream_out=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(st, np.int32), rst[:n])
+    assert np.array_equal(host(fl, np.uint8), rfl[:n])
+    got = host(back, np.uint8)
+    # payload regions as the oracle writes them (the gaps between are untouched: 0xEE)
+    for i in range(n):
+        a, L = int(in_off[i]), int(lens[i])
+        if not np.array_equal(got[a:a + L], rpl[a:a + L]):
+            raise AssertionError(f"frame {i} (len {L}) differs")
+    assert dec.get_peer_nonce(0) == int(peer[0])

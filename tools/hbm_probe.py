@@ -24,6 +24,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--sets", type=int, default=8)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--variants", default="0,8")
+ap.add_argument("--forms", default="bench,clean,warm")
+ap.add_argument("--stream-out", action="store_true", help="decode with ZMQG_OPT_STREAM_OUT (cache hint)")
 ap.add_argument("--no-check", action="store_true", help="(ablated timing builds: outputs are not the codec's)")
 ap.add_argument("--side-prefetch", action="store_true",
                 help="experiment: a reduction over each wire on a second stream, concurrent with its decode")
@@ -104,7 +106,8 @@ def main():
                     side.wait_event(f)
                     with torch.cuda.stream(side):
                         sinks.append(wires[k][: n * W // 8 * 8].view(torch.int64).max())
-                dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream, max_len=W)
+                dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream, max_len=W,
+                                 stream_out=a.stream_out)
             e1.record(stream)
             return e0, e1
 
@@ -114,41 +117,49 @@ def main():
             for k in range(K):
                 assert int((sts[k] != 0).sum()) == 0 and torch.equal(backs[k], pays[k])
 
-        res = {"bench": [], "clean": [], "warm": []}
+        forms = a.forms.split(",")
+        res = {f: [] for f in forms}
         for r in range(a.reps + 1):
-            encs()
-            e0, e1 = decs()
-            torch.cuda.synchronize()
-            check()
-            if r:
-                res["bench"].append(e0.elapsed_time(e1) * 1e3 / K)
-            encs()
-            s = sweep.sum()  # clean lines in the cache
-            e0, e1 = decs()
-            torch.cuda.synchronize()
-            check()
-            del s
-            if r:
-                res["clean"].append(e0.elapsed_time(e1) * 1e3 / K)
-            # warm: encode k then decode k, the decode alone timed
-            t = 0.0
-            for k in range(K):
-                sts[k].fill_(-1)
-                enc.encode_batch(sid, None, flags, in_off, lens, pays[k], out_off, wires[k], stream, max_len=P,
-                                 nonce_auto=True)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream, max_len=W)
-                e1.record(stream)
+            if "bench" in forms:
+                encs()
+                e0, e1 = decs()
                 torch.cuda.synchronize()
-                t += e0.elapsed_time(e1) * 1e3
-            check()
-            if r:
-                res["warm"].append(t / K)
+                check()
+                if r:
+                    res["bench"].append(e0.elapsed_time(e1) * 1e3 / K)
+            if "clean" in forms:
+                encs()
+                s = sweep.sum()  # clean lines in the cache
+                e0, e1 = decs()
+                torch.cuda.synchronize()
+                check()
+                del s
+                if r:
+                    res["clean"].append(e0.elapsed_time(e1) * 1e3 / K)
+            if "warm" in forms:
+                # encode k then decode k, the decode alone timed
+                t = 0.0
+                for k in range(K):
+                    sts[k].fill_(-1)
+                    enc.encode_batch(sid, None, flags, in_off, lens, pays[k], out_off, wires[k], stream, max_len=P,
+                                     nonce_auto=True)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream,
+                                     max_len=W)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    t += e0.elapsed_time(e1) * 1e3
+                check()
+                if r:
+                    res["warm"].append(t / K)
         print(f"variant G={v}: " + "  ".join(f"{k} {min(x):6.1f}/{sorted(x)[len(x) // 2]:6.1f} us"
                                              for k, x in res.items()) + "  (decode per launch, min/median)")
         enc.close()
         dec.close()
+    import json
+    sid_, commit = C.build_id()
+    print(json.dumps({"build": {"source_id": sid_, "commit": commit}}))
 
 
 if __name__ == "__main__":

@@ -38,9 +38,9 @@ def build_of(log):
     raise ValueError(f"no bench line in {log}")
 
 
-builds = {build_of(f)["source_id"]: build_of(f) for f in
-          glob.glob(f"{root}/pmcv/run.log") + glob.glob(f"{root}/pmcs/run.log") + glob.glob(f"{root}/pmct/fetch.log")
-          + glob.glob(f"{root}/pmct/write.log")}
+logs = (glob.glob(f"{root}/pmcv/run.log") + glob.glob(f"{root}/pmcs/run.log")
+        + glob.glob(f"{root}/pmct/resident/*/run.log") + glob.glob(f"{root}/pmct/hbm/*/run.log"))
+builds = {build_of(f)["source_id"]: build_of(f) for f in logs}
 assert len(builds) == 1, f"PMC passes of different builds: {sorted(builds)}"
 build = next(iter(builds.values()))
 
@@ -49,16 +49,23 @@ try:
     stall = json.load(open(f"{root}/pmcs/summary.json"))
 except FileNotFoundError:
     stall = {}
-fetch, write = per_kernel(f"{root}/pmct/fetch"), per_kernel(f"{root}/pmct/write")
-fcal, wcal = per_kernel(f"{root}/pmct/fetch_cal"), per_kernel(f"{root}/pmct/write_cal")
-cal_f, _ = pick(fcal, r"k_copy<false, 1>", "FETCH_SIZE")
-cal_w, _ = pick(wcal, r"k_copy<false, 1>", "WRITE_SIZE")
+fcal, wcal = per_kernel(f"{root}/pmct/cal/fetch"), per_kernel(f"{root}/pmct/cal/write")
 moved_kib = N * P / 1024
+# the frame kernels' reads: LDS-DMA of whole 16-byte granules in runs of a
+# frame's five (k_frames_seq's staged input, k_frames_lds) -- the
+# calibration copy's cooperative shape (4 lanes per frame window); writes:
+# each lane's own 64-byte pieces -- the lane shape
+cal_f, _ = pick(fcal, r"k_copy<true, 1>", "FETCH_SIZE")
+cal_w, _ = pick(wcal, r"k_copy<false, 1>", "WRITE_SIZE")
+cal_f_lane, _ = pick(fcal, r"k_copy<false, 1>", "FETCH_SIZE")
 scale = moved_kib / cal_f
-out_t, out_v = {}, {}
-for dec in (True, False):
+EA = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum")
+
+
+def traffic(form, dec):
     tag = "decode" if dec else "encode"
     pat = r"k_frames\w*<%s" % ("true" if dec else "false")
+    fetch, write = per_kernel(f"{root}/pmct/{form}/fetch"), per_kernel(f"{root}/pmct/{form}/write")
     f, kname = pick(fetch, pat, "FETCH_SIZE")
     w, _ = pick(write, pat, "WRITE_SIZE")
     kshort = re.search(r"(k_frames\w*)<", kname).group(1) + "<%s>" % tag
@@ -66,7 +73,25 @@ for dec in (True, False):
     alg_w = N * (P + 5) if dec else N * (P + 33)
     t = {"kernel": kshort, "read_bytes_per_launch": f * scale * 1024, "write_bytes_per_launch": w * 1024,
          "fetch_size_kib_raw": f, "write_size_kib_raw": w, "algorithmic_read_bytes_per_launch": alg_r,
-         "algorithmic_write_bytes_per_launch": alg_w}
+         "algorithmic_write_bytes_per_launch": alg_w,
+         "read_vs_algorithmic": f * scale * 1024 / alg_r, "write_vs_algorithmic": w * 1024 / alg_w}
+    ea = per_kernel(f"{root}/pmct/{form}/ea")
+    reqs = {}
+    for c in EA:
+        try:
+            reqs[c] = pick(ea, pat, c)[0]
+        except KeyError:
+            pass
+    if reqs:
+        t["l2_memory_side_requests_per_launch"] = reqs
+    return t
+
+
+out_t, out_v = {}, {}
+for dec in (True, False):
+    tag = "decode" if dec else "encode"
+    t = traffic("resident", dec)
+    kshort = t["kernel"]
     v = valu["k_frames<%s>" % tag]
     vv = {"kernel": kshort, "valu_wave_instr_per_launch": v["SQ_INSTS_VALU"], "salu_instr_per_launch": v["SQ_INSTS_SALU"],
           "vmem_instr_per_launch": v["SQ_INSTS_VMEM"], "waves": v["SQ_WAVES"],
@@ -85,18 +110,25 @@ for dec in (True, False):
     else:
         out_t["encode"] = t
         out_v["encode"] = vv
+out_t["hbm_fed"] = {"decode": traffic("hbm", True), "encode": traffic("hbm", False),
+                    "form": "tools/hbm_probe.py --forms bench: 8 config-2 batches with their own buffers, 8 encodes "
+                            "back to back then their 8 decodes (bench.py hbm_fed's order); every input from HBM"}
 out_t.update({
     "source_id": build["source_id"], "commit": build["commit"],
     "workload": "config2: 65536 x 1024 B frames, one session, one lane per frame (1024 waves, 1 per SIMD)",
-    "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace) of python bench.py "
-              "--eager --steps 3 --warmup 1 (tools/pmc_traffic.sh via tools/pmc_profiles.sh); calibration: the same "
-              "counters over tools/framecopy (65536 x 1024 B, LANE shape, known bytes); tools/pmc_profiles.py",
-    "units": "bytes per launch", "fetch_scale": scale,
-    "fetch_scale_note": "FETCH_SIZE under-reports this access shape on gfx950 (MI355X_MICROARCH.md HBM section): "
-                        "the calibration copy reads %.0f KiB reported per %.0f KiB moved, so reads are scaled by "
-                        "%.3f.  WRITE_SIZE is taken as reported; the calibration copy's lane stores show %.2fx "
-                        "the bytes moved (partial-line writes), the same kind of amplification as the frame kernel."
-                        % (cal_f, moved_kib, scale, cal_w / moved_kib)})
+    "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_EA0_{RDREQ,RDREQ_32B,WRREQ,WRREQ_64B}_sum (separate "
+              "passes, --kernel-trace) of python bench.py --eager --steps 3 --warmup 1 --no-deployable --hbm-sets 0 "
+              "(MALL-resident, top level) and of tools/hbm_probe.py --forms bench (hbm_fed); calibration: the same "
+              "counters over tools/framecopy (65536 x 1024 B, known bytes); tools/pmc_traffic.sh, "
+              "tools/pmc_profiles.py",
+    "units": "bytes per launch; request counts per launch", "fetch_scale": scale,
+    "fetch_scale_note": "FETCH_SIZE under-reports on gfx950 (MI355X_MICROARCH.md HBM section): the calibration "
+                        "copy's cooperative shape (the frame kernels' LDS-DMA granule runs) reads %.0f KiB "
+                        "reported per %.0f KiB moved (the lane shape %.0f), so reads are scaled by %.3f.  "
+                        "WRITE_SIZE is taken as reported; the calibration copy's lane stores show %.2fx the bytes "
+                        "moved.  FETCH_SIZE counts the L2's memory-side requests, Infinity-Cache hits included: "
+                        "the resident form's reads mostly hit the MALL, the HBM-fed form's come from HBM."
+                        % (cal_f, moved_kib, cal_f_lane, scale, cal_w / moved_kib)})
 out_v.update({
     "source_id": build["source_id"], "commit": build["commit"],
     "workload": out_t["workload"],
