@@ -74,6 +74,8 @@ def parse():
     p.add_argument("--hbm-sets", type=int, default=8,
                    help="config-2 batches of the HBM-fed form (hbm_fed): each its own payload, wire and result "
                         "buffers, so no kernel reads what the Infinity Cache still holds (0: skip)")
+    p.add_argument("--stream-out", action="store_true",
+                   help="experiment: the main line's decodes with ZMQG_OPT_STREAM_OUT")
     p.add_argument("--no-deployable", action="store_true",
                    help="skip host_paths' deployable paths (the engine-hook bench and the libzmq CURVE pairs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -183,7 +185,8 @@ def main():
 
     def step(st):
         step_enc(st)
-        dec.decode_batch(sid, out_off, wlen, wire, in_off, back, fl_out, st_out, st, max_len=W)
+        dec.decode_batch(sid, out_off, wlen, wire, in_off, back, fl_out, st_out, st, max_len=W,
+                         stream_out=args.stream_out)
 
     for _ in range(args.warmup):
         step(stream)

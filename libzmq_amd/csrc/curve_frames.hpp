@@ -1446,8 +1446,16 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     // round trip (form 1, read back and stored at once, costs the resident
     // decode ~8 us per launch)
     bool cs_pend = false; // the staging area holds the previous step's chunks
-    __shared__ __attribute__((aligned(16))) uint8_t sq_stg[ZMQG_SEQ_COOPST && SO ? kFramesWaves * 64 * 64 : 16];
-    uint8_t *const stg = sq_stg + (ZMQG_SEQ_COOPST && SO ? (threadIdx.x >> 6) * 64u * 64u : 0u);
+    // Layout granule-major (granule k of lane l's chunk at kStgPlane k + 16 l,
+    // each plane padded by 16 bytes): a lane's four writes are four
+    // conflict-free instructions (consecutive lanes, consecutive 16 bytes)
+    // instead of 64-byte strides that put every lane on the same eight banks
+    constexpr uint32_t kStgPlane = 64u * 16u + 16u;
+    __shared__ __attribute__((aligned(16))) uint8_t sq_stg[ZMQG_SEQ_COOPST && SO ? kFramesWaves * 4 * kStgPlane : 16];
+    uint8_t *const stg = sq_stg + (ZMQG_SEQ_COOPST && SO ? (threadIdx.x >> 6) * 4u * kStgPlane : 0u);
+    auto stg_put = [&](uint32_t k) { return stg + kStgPlane * k + 16u * lane; };
+    // store j of this lane: granule lane % 4 of frame 16 j + lane / 4
+    auto stg_get = [&](uint32_t j) { return stg + kStgPlane * (lane & 3u) + 16u * (16u * j + (lane >> 2)); };
     uint64_t cs_dst[4];
     uint32_t cs_nw[4];
     // (SO: the ZMQG_OPT_STREAM_OUT instantiation; al64 is wave-uniform)
@@ -1571,7 +1579,7 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
-                cg[j] = *(const u32x4 *) (stg + 64u * (16u * j + (lane >> 2)) + 16u * (lane & 3u));
+                cg[j] = *(const u32x4 *) stg_get(j);
             if (ZMQG_SEQ_COOPST == 3) { // stored here, a whole keystream ahead of the next step's wait
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
@@ -1730,18 +1738,18 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // (after this step's reads)
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    *(u32x4 *) (stg + 64u * lane + 16u * k) = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                    *(u32x4 *) stg_put(k) = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
                 cs_pend = true;
             } else if (ZMQG_SEQ_COOPST == 1 && coop && __builtin_amdgcn_ballot_w64(lastw) == 0) {
                 // (no lane on its last window: every active frame's chunk is whole)
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    *(u32x4 *) (stg + 64u * lane + 16u * k) = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                    *(u32x4 *) stg_put(k) = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 u32x4 g[4];
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
-                    g[j] = *(const u32x4 *) (stg + 64u * (16u * j + (lane >> 2)) + 16u * (lane & 3u));
+                    g[j] = *(const u32x4 *) stg_get(j);
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
                     if (t < cs_nw[j])
