@@ -3,7 +3,7 @@
 # tools/zmtp_bench.py twice and once under a kernel trace.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-mkdir -p gpurun_out/zr
+mkdir -p gpurun_out/zr; rm -rf gpurun_out/zr/prof
 timeout -k 10 300 python -u -m pytest tests/test_zmtp.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/zr/pytest.log 2>&1 || { tail -30 gpurun_out/zr/pytest.log; exit 1; }
 tail -1 gpurun_out/zr/pytest.log
 ZMQG_ZMTP_CUB=1 timeout -k 10 300 python -u -m pytest tests/test_zmtp.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/zr/pytest_cub.log 2>&1 || { tail -30 gpurun_out/zr/pytest_cub.log; exit 1; }

@@ -111,8 +111,9 @@ for dec in (True, False):
         out_t["encode"] = t
         out_v["encode"] = vv
 out_t["hbm_fed"] = {"decode": traffic("hbm", True), "encode": traffic("hbm", False),
-                    "form": "tools/hbm_probe.py --forms bench: 8 config-2 batches with their own buffers, 8 encodes "
-                            "back to back then their 8 decodes (bench.py hbm_fed's order); every input from HBM"}
+                    "form": "tools/hbm_probe.py --forms bench --stream-out: 8 config-2 batches with their own buffers, "
+                            "8 encodes back to back then their 8 decodes with ZMQG_OPT_STREAM_OUT (bench.py hbm_fed); "
+                            "every input from HBM"}
 out_t.update({
     "source_id": build["source_id"], "commit": build["commit"],
     "workload": "config2: 65536 x 1024 B frames, one session, one lane per frame (1024 waves, 1 per SIMD)",

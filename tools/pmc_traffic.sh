@@ -1,7 +1,8 @@
 #!/bin/bash
 # HBM traffic of config 2's frame kernels in both forms -- MALL-resident
 # (bench.py --eager, the main line alone) and HBM-fed (tools/hbm_probe.py
-# --forms bench: 8 batches with their own buffers) -- one rocprofv3 pass per
+# --forms bench --stream-out: 8 batches with their own buffers, decoded with
+# ZMQG_OPT_STREAM_OUT as bench.py hbm_fed does) -- one rocprofv3 pass per
 # counter group, kernel-trace only (MI355X_MICROARCH.md HBM section):
 # FETCH_SIZE; WRITE_SIZE; the L2's memory-side request counts TCC_EA0_RDREQ /
 # _RDREQ_32B / _WRREQ / _WRREQ_64B.  Then FETCH_SIZE and WRITE_SIZE over
@@ -29,7 +30,7 @@ for form in resident hbm; do
         --no-deployable --hbm-sets 0 > $O/$form/$p/run.log 2>&1 || { echo "$form $p failed"; tail -5 $O/$form/$p/run.log; exit 1; }
     else
       timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $O/$form/$p -o pmc -- \
-        python tools/hbm_probe.py --variants 0 --reps 1 --forms bench > $O/$form/$p/run.log 2>&1 || { echo "$form $p failed"; tail -5 $O/$form/$p/run.log; exit 1; }
+        python tools/hbm_probe.py --variants 0 --reps 1 --forms bench --stream-out > $O/$form/$p/run.log 2>&1 || { echo "$form $p failed"; tail -5 $O/$form/$p/run.log; exit 1; }
     fi
   done
 done
