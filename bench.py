@@ -38,7 +38,10 @@ JSON line fields beyond the driver contract:
                 PUSH/PULL pairs, stock against the batched GPU codec.
   hbm_fed       config 2 with every kernel input read from HBM (K batches with
                 their own buffers, beyond the 256 MiB Infinity Cache), with
-                its own decode roofline.
+                its own decode roofline and PMC traffic; its decodes pass
+                ZMQG_OPT_STREAM_OUT, the store hint for outputs no cache
+                holds (--stream-out applies it to the main line too, for
+                comparison).
   cpu_baseline  kind "reference": the stock libzmq build's curve_encoding_t
                 on the host cores, rank 0 at N=1 only, on a bounded sample;
                 beside it ("port") the oracle's C restatement of the framing
