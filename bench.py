@@ -205,10 +205,11 @@ def main():
     # launch: the host's per-kernel launch cost stays out of the timed region.
     # HIP events cannot time kernels inside a graph, so the per-launch kernel
     # durations (roofline) come from graph replays just before the timed one
-    # (graph_shares).  An eager pass of K more steps after the timed replay,
-    # with the ctx profiling hooks on, gives eager_ms_per_step and the call
-    # spans (roofline.hooked_eager).  --eager times the eager steps (events
-    # on) instead.
+    # (graph_shares).  An eager pass of K more steps right after the timed
+    # replay gives eager_ms_per_step (host-launched calls, hooks off), and a
+    # second one with the ctx profiling hooks on the call spans
+    # (roofline.hooked_eager).  --eager times the eager steps (events on)
+    # instead.
     graph = None
     if not args.eager:
         try:
@@ -276,18 +277,25 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    if graph is not None:  # the replayed work is correct too
-        assert int((st_out != 0).sum()) == 0 and torch.equal(back, payload), "graph replay mismatch"
     eager_elapsed = None
     if graph is not None:
-        enc.set_profiling(True)
-        dec.set_profiling(True)
-        torch.cuda.synchronize(dev)
+        # the same K steps launched from the host call by call (what a caller
+        # without a graph gets), right after the timed replay while the clock
+        # is still up, the profiling hooks off (their event pairs add a
+        # dispatch each); host clock
         e0 = time.perf_counter()
         for _ in range(args.steps):
             step(stream)
         torch.cuda.synchronize(dev)
         eager_elapsed = time.perf_counter() - e0
+    if graph is not None:  # the replayed (and eager) work is correct too
+        assert int((st_out != 0).sum()) == 0 and torch.equal(back, payload), "graph replay mismatch"
+        # the call spans of roofline.hooked_eager: one more eager pass, hooks on
+        enc.set_profiling(True)
+        dec.set_profiling(True)
+        for _ in range(args.steps):
+            step(stream)
+        torch.cuda.synchronize(dev)
     from libzmq_amd import shard
     elapsed = shard.max_over_ranks(elapsed)  # the slowest rank times the job
     # the eager pass's event pairs (the hooks were off during the capture)
