@@ -8,6 +8,8 @@
 //   zscan    the library's k_zmtp_scan on a config-2-like stream (1,066-byte
 //            LARGE frames of random bytes);
 //   zscanpX  k_zmtp_scan_p, the persistent form, X x CUs workgroups;
+//   vzV      variants of the signature tests (vz_scan_tile below), checked
+//            candidate for candidate against zscan;
 // each timed with hip events over 20 back-to-back launches (the buffer stays
 // MALL-resident between them) and after a 1 GB sweep (HBM-fed).
 //   hipcc -O3 --offload-arch=gfx950 -o tools/bin/scan_probe tools/scan_probe.hip
@@ -109,6 +111,128 @@ __global__ void k_fill_frames(uint8_t *b, uint64_t n)
     }
 }
 
+// Variants of zmtp_scan_tile's signature tests, for
+// timing against the library's: V = 1 one first-word compare per position
+// and no per-word 0x07 filter; V = 2 the library's filter without the
+// per-position bound (bytes past n load as zero and cannot match
+// "\x07MESSAGE"); V = 3 = V1 with the header's size taken by byte swaps.
+template <int O, int NW>
+__device__ __forceinline__ uint32_t vz_word(const uint32_t (&w)[NW])
+{ // bytes [O, O + 4) of the window, little-endian
+    if constexpr (O % 4 == 0)
+        return w[O / 4];
+    else
+        return __builtin_amdgcn_alignbyte(w[O / 4 + 1], w[O / 4], O % 4);
+}
+template <int O, int NW>
+__device__ __forceinline__ uint64_t vz_cand_fast(const uint32_t (&w)[NW], uint64_t qq, uint64_t n, int64_t max_msg)
+{
+    if (qq >= 9 && (zmqg::zmtp_byte<O - 9>(w) & zmqg::kZmtpLarge)) {
+        const uint64_t size = ((uint64_t) __builtin_bswap32(vz_word<O - 8>(w)) << 32) | __builtin_bswap32(vz_word<O - 4>(w));
+        const uint64_t p = qq - 9;
+        if (zmqg::zmtp_size_ok(size, max_msg) && size >= 8 && size <= n - p - 9)
+            return p;
+    }
+    if (qq >= 2 && !(zmqg::zmtp_byte<O - 2>(w) & zmqg::kZmtpLarge)) {
+        const uint64_t size = zmqg::zmtp_byte<O - 1>(w), p = qq - 2;
+        if (zmqg::zmtp_size_ok(size, max_msg) && size >= 8 && size <= n - p - 2)
+            return p;
+    }
+    return zmqg::kZmtpNone;
+}
+
+template <int V>
+__device__ __forceinline__ void vz_scan_tile(uint64_t n, int64_t max_msg, uint64_t tile,
+                                             const uint32_t (&w)[zmqg::kZmtpRounds][10], uint64_t *cand_wg,
+                                             uint64_t *count_wg, uint16_t *count16)
+{
+    using namespace zmqg;
+    constexpr uint32_t R = kZmtpRounds;
+    const uint64_t wg0 = tile * kZmtpWgBytes;
+    uint64_t *const dst0 = cand_wg + (size_t) tile * kZmtpWgCap;
+    uint64_t f[R][2];
+    uint32_t cnt[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+        const uint64_t base = wg0 + 16ull * (k * kZmtpThreads + threadIdx.x);
+        uint64_t f0 = 0, f1 = 0;
+        uint32_t c = 0;
+        auto at = [&](uint64_t p) {
+            if (p != kZmtpNone && c < 2u) {
+                f1 = c ? p : f1;
+                f0 = c ? f0 : p;
+                ++c;
+            }
+        };
+        const uint32_t(&wk)[10] = w[k];
+#define VZ_CAND(O, q) (V == 3 ? vz_cand_fast<O>(wk, q, n, max_msg) : zmtp_cand_at<O>(wk, q, n, max_msg))
+#define VZ_SIG1(Q, J)                                                                                            \
+    if (__builtin_amdgcn_alignbyte(wk[5 + Q], wk[4 + Q], J) == 0x53454d07u)                                      \
+        if (__builtin_amdgcn_alignbyte(wk[6 + Q], wk[5 + Q], J) == 0x45474153u)                                  \
+            at(VZ_CAND(16 + 4 * Q + J, base + 4 * Q + J));
+#define VZ_SIG2(Q, J)                                                                                            \
+    if (__builtin_amdgcn_alignbyte(wk[5 + Q], wk[4 + Q], J) == 0x53454d07u &&                                    \
+        __builtin_amdgcn_alignbyte(wk[6 + Q], wk[5 + Q], J) == 0x45474153u)                                      \
+        at(zmtp_cand_at<16 + 4 * Q + J>(wk, base + 4 * Q + J, n, max_msg));
+#define VZ_WORD(Q)                                                                                               \
+    if constexpr (V == 2) {                                                                                      \
+        const uint32_t x = wk[4 + Q] ^ 0x07070707u;                                                              \
+        if ((x - 0x01010101u) & ~x & 0x80808080u) {                                                              \
+            VZ_SIG2(Q, 0)                                                                                        \
+            VZ_SIG2(Q, 1)                                                                                        \
+            VZ_SIG2(Q, 2)                                                                                        \
+            VZ_SIG2(Q, 3)                                                                                        \
+        }                                                                                                        \
+    } else {                                                                                                     \
+        VZ_SIG1(Q, 0)                                                                                            \
+        VZ_SIG1(Q, 1)                                                                                            \
+        VZ_SIG1(Q, 2)                                                                                            \
+        VZ_SIG1(Q, 3)                                                                                            \
+    }
+        VZ_WORD(0)
+        VZ_WORD(1)
+        VZ_WORD(2)
+        VZ_WORD(3)
+#undef VZ_WORD
+#undef VZ_SIG1
+#undef VZ_SIG2
+#undef VZ_CAND
+        f[k][0] = f0;
+        f[k][1] = f1;
+        cnt[k] = c;
+    }
+    uint64_t packed = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k)
+        packed |= (uint64_t) cnt[k] << (16 * k);
+    uint64_t tot;
+    const uint64_t ex = zmtp_block_excl4(packed, tot);
+    uint32_t base_out = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+        const uint32_t off = base_out + (uint32_t) ((ex >> (16 * k)) & 0xffffu);
+        if (cnt[k] > 0u)
+            dst0[off] = f[k][0];
+        if (cnt[k] > 1u)
+            dst0[off + 1] = f[k][1];
+        base_out += (uint32_t) ((tot >> (16 * k)) & 0xffffu);
+    }
+    if (threadIdx.x == 0) {
+        count_wg[tile] = base_out;
+        count16[tile] = (uint16_t) base_out;
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(zmqg::kZmtpThreads) void k_vz_scan(const uint8_t *b, uint64_t n, int64_t max_msg,
+                                                                uint64_t *cand_wg, uint64_t *count_wg,
+                                                                uint16_t *count16)
+{
+    uint32_t w[zmqg::kZmtpRounds][10];
+    zmqg::zmtp_scan_load(b, n, blockIdx.x, w);
+    vz_scan_tile<V>(n, max_msg, blockIdx.x, w, cand_wg, count_wg, count16);
+}
+
 int main()
 {
     const uint64_t n = 65536ull * 1066ull;
@@ -125,17 +249,18 @@ int main()
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    uint64_t *cand_wg = nullptr, *count_wg = nullptr, *count_ref = nullptr;
+    uint64_t *cand_wg = nullptr, *count_wg = nullptr, *count_ref = nullptr, *cand_ref = nullptr;
     uint16_t *count16 = nullptr;
     CK(hipMalloc(&cand_wg, 8ull * g * zmqg::kZmtpWgCap));
     CK(hipMalloc(&count_wg, 8ull * (g + 1)));
+    CK(hipMalloc(&cand_ref, 8ull * g * zmqg::kZmtpWgCap));
     CK(hipMalloc(&count_ref, 8ull * (g + 1)));
     CK(hipMalloc(&count16, 2ull * (g + 8)));
     for (int mode = 0; mode < 2; ++mode) {
-        for (int kind = 0; kind < 7; ++kind) {
+        for (int kind = 0; kind < 10; ++kind) {
             if (kind == 3) { // the frame stream for the library's scans
                 hipLaunchKernelGGL(k_fill_frames, dim3(4096), dim3(256), 0, 0, b, n);
-                hipLaunchKernelGGL(zmqg::k_zmtp_scan, dim3(g), dim3(kT), 0, 0, b, n, (int64_t) -1, cand_wg, count_ref,
+                hipLaunchKernelGGL(zmqg::k_zmtp_scan, dim3(g), dim3(kT), 0, 0, b, n, (int64_t) -1, cand_ref, count_ref,
                                    count16);
                 CK(hipDeviceSynchronize());
             }
@@ -154,6 +279,15 @@ int main()
                 else if (kind == 3)
                     hipLaunchKernelGGL(zmqg::k_zmtp_scan, dim3(g), dim3(kT), 0, 0, b, n, (int64_t) -1, cand_wg,
                                        count_wg, count16);
+                else if (kind == 7)
+                    hipLaunchKernelGGL(k_vz_scan<1>, dim3(g), dim3(kT), 0, 0, b, n, (int64_t) -1, cand_wg, count_wg,
+                                       count16);
+                else if (kind == 8)
+                    hipLaunchKernelGGL(k_vz_scan<2>, dim3(g), dim3(kT), 0, 0, b, n, (int64_t) -1, cand_wg, count_wg,
+                                       count16);
+                else if (kind == 9)
+                    hipLaunchKernelGGL(k_vz_scan<3>, dim3(g), dim3(kT), 0, 0, b, n, (int64_t) -1, cand_wg, count_wg,
+                                       count16);
                 else
                     hipLaunchKernelGGL(zmqg::k_zmtp_scan_p, dim3((kind == 4 ? 2 : kind == 5 ? 4 : 6) * cus), dim3(kT), 0,
                                        0, b, n, (int64_t) -1, (uint64_t) g, cand_wg, count_wg, count16);
@@ -175,8 +309,18 @@ int main()
                     fprintf(stderr, "kind %d: counts differ (total %llu)\n", kind, (unsigned long long) tot);
                     return 1;
                 }
+                if (kind >= 7) { // and the same candidates
+                    std::vector<uint64_t> c1((size_t) g * zmqg::kZmtpWgCap), c2((size_t) g * zmqg::kZmtpWgCap);
+                    CK(hipMemcpy(c1.data(), cand_ref, 8ull * c1.size(), hipMemcpyDeviceToHost));
+                    CK(hipMemcpy(c2.data(), cand_wg, 8ull * c2.size(), hipMemcpyDeviceToHost));
+                    for (uint32_t i = 0; i < g; ++i)
+                        if (memcmp(&c1[(size_t) i * zmqg::kZmtpWgCap], &c2[(size_t) i * zmqg::kZmtpWgCap], 8ull * h1[i])) {
+                            fprintf(stderr, "kind %d: candidates differ in tile %u\n", kind, i);
+                            return 1;
+                        }
+                }
             }
-            static const char *names[] = {"plain", "scan3", "wide", "zscan", "zscanp2", "zscanp4", "zscanp6"};
+            static const char *names[] = {"plain", "scan3", "wide", "zscan", "zscanp2", "zscanp4", "zscanp6", "vz1", "vz2", "vz3"};
             printf("%-6s %-9s best %7.1f us  mean %7.1f us  %6.2f TB/s (best)\n", names[kind],
                    mode ? "hbm-fed" : "resident", best * 1e3, sum / reps * 1e3, n / (best * 1e-3) / 1e12);
         }
