@@ -4,7 +4,8 @@ and decoder loop, src/v3_1_encoder.cpp:23-60, src/v2_decoder.cpp:35-140)
 combined with the CURVE oracle.  Cases follow the decoder's branches: short
 and LARGE sizes (the 255-byte boundary, LARGE with a small size), EMSGSIZE,
 incomplete header / body at the buffer end, a non-MESSAGE frame, planted
-"\\x07MESSAGE" signatures inside bodies, max_frames."""
+"\\x07MESSAGE" signatures inside bodies, max_frames, random bytes seeded with frame-like
+candidates (alone and behind valid frames)."""
 import struct
 import zlib
 
@@ -104,6 +105,13 @@ def _stream_case(rng, case, precom, n=400):
     stream = b"".join(frames)
     if case == "truncated":
         stream = stream[:int(rng.integers(len(stream) // 2, len(stream) - 1))]
+    if case in ("garbage", "garbage_tail"):
+        # random bytes (alone, or after the valid frames) seeded with
+        # frame-like headers + signatures: candidates the walk must not take
+        junk = bytearray(rng.bytes(40000))
+        for k in rng.integers(0, len(junk) - 20, 200):
+            junk[k:k + 11] = bytes([0, int(rng.integers(8, 64))]) + b"\x07MESSAGE" + b"\x00"
+        stream = bytes(junk) if case == "garbage" else stream + bytes(junk)
     if case == "emsgsize":
         max_msg = 2000
     if case == "max_frames":
@@ -123,7 +131,8 @@ def _stream_case(rng, case, precom, n=400):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["clean", "truncated", "planted", "flood", "large_small", "ping", "emsgsize",
                                   "max_frames", "zmtp_flags", "sparse", "planted+cub", "sparse+cub",
-                                  "zmtp_flags+g0", "zmtp_flags+g8", "ping+g0", "ping+g8"])
+                                  "zmtp_flags+g0", "zmtp_flags+g8", "ping+g0", "ping+g8", "garbage",
+                                  "garbage_tail"])
 def test_decode_zmtp_matches_oracle(torch_cuda, C, case, monkeypatch):
     """+cub: the candidate counts scanned by hipCUB (the form for streams above
     128 MiB, ZMQG_ZMTP_CUB forces it).  +g0 / +g8: the decode's frame kernel
@@ -215,3 +224,76 @@ def test_decode_zmtp_matches_oracle(torch_cuda, C, case, monkeypatch):
         assert st[-1] != 0 and (st[:-1] == 0).all()
     if case == "emsgsize":
         assert ref["error"] == Z.EMSGSIZE
+
+
+@pytest.mark.gpu
+def test_zmtp_round_trip_config2(torch_cuda, C):
+    """BASELINE config 2's shape (65,536 x 1 KiB, one session) through the
+    framed path, checked by size-independent properties: encode_zmtp then
+    decode_zmtp returns every payload, flag and frame offset; a ciphertext
+    byte flipped in three frames fails exactly those three; a stream cut
+    inside the last frame stops the parse before it.  The oracle checks the
+    first frames' bytes."""
+    torch = torch_cuda
+    dev = torch.device("cuda", 0)
+    n, P = 65536, 1024
+    W, F = P + 33, P + 33 + 9
+    rng = np.random.default_rng(11)
+    precom = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    inp = torch.randint(0, 256, (n * P,), dtype=torch.uint8, device=dev, generator=g)
+    sid = torch.zeros(n, dtype=torch.int32, device=dev)
+    nonce = torch.arange(3, 3 + n, dtype=torch.int64, device=dev)
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    in_off = torch.arange(n, dtype=torch.int64, device=dev) * P
+    lens = torch.full((n,), P, dtype=torch.int32, device=dev)
+    enc = C.CurveContext(0, 1)
+    enc.session_set(0, precom, C.CLIENT_PREFIX, C.SERVER_PREFIX)
+    stream = torch.empty(n * F + 64, dtype=torch.uint8, device=dev)
+    foff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    enc.encode_zmtp(sid, nonce, flags, in_off, lens, inp, stream, foff)
+    torch.cuda.synchronize()
+    assert int(foff[n]) == n * F
+    assert torch.equal(foff[:n], torch.arange(n, dtype=torch.int64, device=dev) * F)
+    # the first frames against the oracle
+    k = 8
+    h = inp[:k * P].cpu().numpy()
+    sessions = O.make_sessions([precom])
+    ref = O.encode_batch(sessions, np.zeros(k, np.uint32), np.arange(3, 3 + k, dtype=np.uint64), np.zeros(k, np.uint8),
+                         np.arange(k, dtype=np.uint64) * P, np.full(k, P, np.uint32), h,
+                         np.arange(k, dtype=np.uint64) * W, k * W)
+    want = b"".join(Z.frame(ref[i * W:(i + 1) * W]) for i in range(k))
+    assert stream[:k * F].cpu().numpy().tobytes() == want
+
+    def decode(buf, nbytes):
+        dec = C.CurveContext(0, 1)
+        dec.session_set(0, precom, C.SERVER_PREFIX, C.CLIENT_PREFIX, False, 2)
+        d = dict(fo=torch.zeros(n, dtype=torch.int64, device=dev), fl=torch.zeros(n, dtype=torch.int32, device=dev),
+                 po=torch.zeros(n, dtype=torch.int64, device=dev), out=torch.empty(n * F, dtype=torch.uint8, device=dev),
+                 mf=torch.zeros(n, dtype=torch.uint8, device=dev), st=torch.full((n,), -1, dtype=torch.int32, device=dev))
+        r = dec.decode_zmtp(0, buf, nbytes, W, n, d["fo"], d["fl"], d["po"], d["out"], d["mf"], d["st"])
+        dec.close()
+        return r, d
+
+    body = torch.arange(n, dtype=torch.int64, device=dev) * F + 9
+    r, d = decode(stream, n * F)
+    assert r == dict(frames=n, consumed=n * F, out_bytes=n * P, error=0)
+    assert torch.equal(d["fo"], body) and torch.equal(d["po"], body)
+    assert bool((d["fl"] == W).all()) and bool((d["st"] == 0).all()) and bool((d["mf"] == 0).all())
+    got = d["out"].view(n, F)[:, 9:9 + P].reshape(-1)
+    assert torch.equal(got, inp)
+    # tampering: one ciphertext byte in three frames
+    bad = [0, 12345, n - 1]
+    t2 = stream.clone()
+    for i in bad:
+        t2[i * F + 9 + 33 + 100] ^= 0x40
+    r, d = decode(t2, n * F)
+    assert r["frames"] == n and r["consumed"] == n * F
+    st = d["st"].cpu().numpy()
+    assert (np.nonzero(st)[0] == bad).all() and (st[bad] == C.ERR_CRYPTOGRAPHIC).all()
+    # a stream cut inside the last frame: n - 1 frames, the rest left for later
+    r, d = decode(stream, n * F - 100)
+    assert r == dict(frames=n - 1, consumed=(n - 1) * F, out_bytes=(n - 1) * P, error=0)
+    assert bool((d["st"][:n - 1] == 0).all())
+    enc.close()
