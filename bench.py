@@ -38,10 +38,10 @@ JSON line fields beyond the driver contract:
                 PUSH/PULL pairs, stock against the batched GPU codec.
   hbm_fed       config 2 with every kernel input read from HBM (K batches with
                 their own buffers, beyond the 256 MiB Infinity Cache), with
-                its own decode roofline and PMC traffic; its decodes pass
-                ZMQG_OPT_STREAM_OUT, the store hint for outputs no cache
-                holds (--stream-out applies it to the main line too, for
-                comparison).
+                its own decode roofline and PMC traffic; its encodes and
+                decodes pass ZMQG_OPT_STREAM_OUT, the store hint for outputs
+                no cache holds (--stream-out applies it to the main line's
+                decodes too, for comparison).
   cpu_baseline  kind "reference": the stock libzmq build's curve_encoding_t
                 on the host cores, rank 0 at N=1 only, on a bounded sample;
                 beside it ("port") the oracle's C restatement of the framing
@@ -558,7 +558,7 @@ def hbm_fed(torch, dev, stream, enc, dec, K, n, W, P, sid, flags, in_off, lens, 
         ev[0].record(stream)
         for k in range(K):
             enc.encode_batch(sid, None, flags, in_off, lens, pays[k], out_off, wires[k], stream, max_len=P,
-                             nonce_auto=True)
+                             nonce_auto=True, stream_out=True)
         ev[1].record(stream)
         ev[2].record(stream)
         for k in range(K):
@@ -583,8 +583,8 @@ def hbm_fed(torch, dev, stream, enc, dec, K, n, W, P, sid, flags, in_off, lens, 
            "sets": K, "bytes_per_set": n * (2 * P + W),
            "note": f"{K} config-2 batches with their own buffers ({K * n * (2 * P + W) / 2**20:.0f} MiB against "
                    f"the 256 MiB Infinity Cache): {K} encodes back to back, then their {K} decodes, one event pair "
-                   "each; every input comes from HBM; the decodes pass ZMQG_OPT_STREAM_OUT, the cache hint for "
-                   "outputs no cache holds (whole-segment stores)"}
+                   "each; every input comes from HBM; encodes and decodes pass ZMQG_OPT_STREAM_OUT, the cache hint "
+                   "for outputs no cache holds (staged whole-window stores, 16 frames per store instruction)"}
     del pays, wires, backs
     torch.cuda.empty_cache()
     return out

@@ -1459,12 +1459,15 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
     uint64_t cs_dst[4];
     uint32_t cs_nw[4];
     // (SO: the ZMQG_OPT_STREAM_OUT instantiation; al64 is wave-uniform)
-    const bool coop = ZMQG_SEQ_COOPST && SO && DEC && al64;
+    // (encode, form 2 only: each window's 64 bytes at frame_store's 4-byte-
+    // aligned place, B - up + 64 t; the frame's last window stays per lane)
+    const bool coop = ZMQG_SEQ_COOPST && SO && (DEC ? al64 : ZMQG_SEQ_COOPST == 2);
     if (coop) {
+        const uint64_t cbase = DEC ? (uint64_t) (uintptr_t) dst : B - (((uint32_t) B & 3u) ? ((uint32_t) B & 3u) : 4u);
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
             const uint32_t f = 16u * j + (lane >> 2);
-            cs_dst[j] = shfl_u64((uint64_t) (uintptr_t) dst, f) + 16u * (lane & 3u);
+            cs_dst[j] = shfl_u64(cbase, f) + 16u * (lane & 3u);
             cs_nw[j] = (uint32_t) __shfl((int) nw, (int) f);
         }
     }
@@ -1786,8 +1789,33 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
             for (int k = 0; k < 16; ++k)
                 yp[k] = y[k];
         } else {
-            if (act)
-                frame_store(B, t, S, y, ycarry, t + 1u == nw);
+            const bool lastw = act && t + 1u == nw;
+            if constexpr (!DEC) {
+                if (ZMQG_SEQ_COOPST == 2 && had) { // window t-1 of every frame that was active a step ago
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; ++j)
+                        if (t - 1u < cs_nw[j])
+                            seq_store4(cs_dst[j] + 64ull * (t - 1u), cg[j].x, cg[j].y, cg[j].z, cg[j].w);
+                    cs_pend = false;
+                }
+            }
+            if (!DEC && ZMQG_SEQ_COOPST == 2 && coop && __builtin_amdgcn_ballot_w64(lastw) == 0) {
+                // (no lane on its last window: each active frame's window is
+                // frame_store's whole 64 bytes; a later step stores them)
+                const uint32_t u = (uint32_t) B & 3u, sh = u ? 4u - u : 0u;
+                uint32_t o[16];
+                o[0] = __builtin_amdgcn_alignbyte(y[0], ycarry, sh);
+#pragma unroll
+                for (int k = 1; k < 16; ++k)
+                    o[k] = __builtin_amdgcn_alignbyte(y[k], y[k - 1], sh);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // (after this step's reads)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *(u32x4 *) stg_put(k) = (u32x4){o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                cs_pend = true;
+            } else if (act) {
+                frame_store(B, t, S, y, ycarry, lastw);
+            }
         }
         ycarry = y[15];
         if (t < 8u)

@@ -2255,13 +2255,11 @@ void launch_frames(const zmqg_ctx *ctx, int G, uint32_t n, hipStream_t st, const
         return;
     }
     if (G == 0) {
-        if constexpr (DEC) {
-            if (ctl.stream_out) { // ZMQG_OPT_STREAM_OUT: whole-segment output stores
-                hipLaunchKernelGGL((k_frames_seq<DEC, BigOp, true>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags,
-                                   in_off, len, in, out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out,
-                                   status_out, rp, big, zs, ctl);
-                return;
-            }
+        if (ctl.stream_out) { // ZMQG_OPT_STREAM_OUT: whole-window output stores
+            hipLaunchKernelGGL((k_frames_seq<DEC, BigOp, true>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags,
+                               in_off, len, in, out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out,
+                               status_out, rp, big, zs, ctl);
+            return;
         }
         hipLaunchKernelGGL((k_frames_seq<DEC, BigOp>), grid, dim3(kFramesBS), 0, st, n, sid, nonce, flags, in_off, len, in,
                            out_off, out, sessions, max_sessions, kMaxFrameStream, flags_out, status_out, rp, big, zs,
@@ -2846,6 +2844,7 @@ int zmqg_encode_batch_ex(zmqg_ctx *ctx, uint64_t n, const uint32_t *sid, const u
     if (opts) {
         ctl.enc_status = opts->status_out;
         ctl.max_len = opts->max_len;
+        ctl.stream_out = (opts->flags & ZMQG_OPT_STREAM_OUT) ? 1u : 0u;
         // every frame within the bound fits the frame kernel: no body launch
         ctl.no_body = opts->max_len && opts->max_len <= kMaxFrameStream - 43u; // (no wrap near UINT64_MAX)
     }

@@ -259,9 +259,11 @@ class CurveContext:
         return ctypes.byref(o), o
 
     def encode_batch(self, sid, nonce, flags, in_off, length, inp, out_off, out, stream=None, max_len=0,
-                     status_out=None, nonce_auto=False):
+                     status_out=None, nonce_auto=False, stream_out=False):
+        """stream_out: ZMQG_OPT_STREAM_OUT, the cache hint for outputs the
+        device's caches do not hold."""
         n = int(sid.numel())
-        o = self._opts(max_len, status_out, None, nonce_auto)
+        o = self._opts(max_len, status_out, None, nonce_auto, stream_out=stream_out)
         self._check(_lib.zmqg_encode_batch_ex(self._ctx, n, _ptr(sid), _ptr(nonce), _ptr(flags), _ptr(in_off),
                                               _ptr(length), _ptr(inp), _ptr(out_off), _ptr(out),
                                               o[0] if o else None, _stream_handle(stream)), "zmqg_encode_batch")

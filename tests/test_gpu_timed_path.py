@@ -16,7 +16,9 @@ of the send-nonce pre-pass over many tiles.
 * ZMQG_OPT_STREAM_OUT (decode, a cache hint: whole-segment output stores
   staged through LDS) on the replay batch and on mixed lengths whose payloads
   start 64-byte aligned, so lanes reach their last window at different
-  steps -- the same bytes, statuses and flags as the oracle."""
+  steps -- the same bytes, statuses and flags as the oracle; and on encode
+  (staged 64-byte windows at 4-byte-aligned places) over ragged payloads,
+  packed wire frames and several sessions."""
 import os
 
 import numpy as np
@@ -220,3 +222,45 @@ def test_stream_out_mixed_lengths(torch_cuda, C, variant):
         if not np.array_equal(got[a:a + L], rpl[a:a + L]):
             raise AssertionError(f"frame {i} (len {L}) differs")
     assert dec.get_peer_nonce(0) == int(peer[0])
+
+
+@pytest.mark.parametrize("variant", ["default", "0"])
+def test_stream_out_encode_mixed_lengths(torch_cuda, C, variant):
+    """ZMQG_OPT_STREAM_OUT on encode: the one-lane kernel stages each
+    window's 64 output bytes and stores them a step later, 16 frames per
+    instruction, at frame_store's 4-byte-aligned places; each frame's last
+    window stays per lane.  Payloads of 0 ... 4,400 bytes (and a few for the
+    body kernel) at unaligned input offsets, packed wire frames at every
+    alignment, three sessions, random flags: the whole output buffer against
+    the oracle's sequential encode, bytes past the last frame untouched."""
+    torch = torch_cuda
+    rng = np.random.default_rng(81)
+    n, S = 20000, 3
+    lens = rng.integers(0, 4400, n).astype(np.uint32)
+    lens[::97] = 0
+    lens[7::1999] = rng.integers(5000, 12000, lens[7::1999].size)
+    in_off = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + rng.integers(0, 8, n).astype(np.uint64))[:-1]])
+    in_off = in_off.astype(np.uint64)
+    W_ = lens.astype(np.uint64) + 33
+    out_off = np.concatenate([[0], np.cumsum(W_)[:-1]]).astype(np.uint64)
+    precoms = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(S)]
+    sid = rng.integers(0, S, n).astype(np.uint32)
+    nonce = rng.integers(1, 1 << 40, n).astype(np.uint64)
+    flags = rng.integers(0, 4, n).astype(np.uint8)
+    total = int(in_off[-1] + lens[-1]) + 8
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    wtot = int(out_off[-1] + W_[-1])
+    ref = O.encode_batch(O.make_sessions(precoms), sid, nonce, flags, in_off, lens, inp, out_off, wtot)
+    enc = _ctx(C, variant, S)
+    for s in range(S):
+        enc.session_set(s, precoms[s], O.CLIENT_PREFIX, O.SERVER_PREFIX)
+    out = torch.full((wtot + 256,), 0xEE, dtype=torch.uint8, device="cuda")
+    enc.encode_batch(dev(torch, sid), dev(torch, nonce), dev(torch, flags), dev(torch, in_off), dev(torch, lens),
+                     dev(torch, inp), dev(torch, out_off), out, stream_out=True)
+    torch.cuda.synchronize()
+    got = host(out, np.uint8)
+    assert (got[wtot:] == 0xEE).all()
+    bad = np.nonzero(got[:wtot] != ref[:wtot])[0]
+    if bad.size:
+        f = int(np.searchsorted(out_off, bad[0], side="right")) - 1
+        raise AssertionError(f"{bad.size} bytes differ, first at {bad[0]} (frame {f}, len {lens[f]})")

@@ -10,6 +10,9 @@ span timed by one event pair.  Forms:
 Each form for the decode frame kernels in turn (ZMQG_FRAMES_G: 0 =
 k_frames_seq, 8 = k_frames_lds), every decode checked.
 
+With --time-enc the bench form's K encodes are timed too (--enc-stream-out:
+ZMQG_OPT_STREAM_OUT on them).
+
   hbm_probe.py [--sets 8] [--reps 3]"""
 import argparse
 import os
@@ -26,6 +29,8 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--variants", default="0,8")
 ap.add_argument("--forms", default="bench,clean,warm")
 ap.add_argument("--stream-out", action="store_true", help="decode with ZMQG_OPT_STREAM_OUT (cache hint)")
+ap.add_argument("--enc-stream-out", action="store_true", help="encode with ZMQG_OPT_STREAM_OUT")
+ap.add_argument("--time-enc", action="store_true", help="also time the encodes of the bench form")
 ap.add_argument("--no-check", action="store_true", help="(ablated timing builds: outputs are not the codec's)")
 ap.add_argument("--side-prefetch", action="store_true",
                 help="experiment: a reduction over each wire on a second stream, concurrent with its decode")
@@ -83,9 +88,13 @@ def main():
         _, enc, dec = make(v)
 
         def encs():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
             for k in range(K):
                 enc.encode_batch(sid, None, flags, in_off, lens, pays[k], out_off, wires[k], stream, max_len=P,
-                                 nonce_auto=True)
+                                 nonce_auto=True, stream_out=a.enc_stream_out)
+            e1.record(stream)
+            return e0, e1
 
         def decs():
             for k in range(K):
@@ -119,14 +128,18 @@ def main():
 
         forms = a.forms.split(",")
         res = {f: [] for f in forms}
+        if a.time_enc:
+            res["encode"] = []
         for r in range(a.reps + 1):
             if "bench" in forms:
-                encs()
+                c0, c1 = encs()
                 e0, e1 = decs()
                 torch.cuda.synchronize()
                 check()
                 if r:
                     res["bench"].append(e0.elapsed_time(e1) * 1e3 / K)
+                    if a.time_enc:
+                        res["encode"].append(c0.elapsed_time(c1) * 1e3 / K)
             if "clean" in forms:
                 encs()
                 s = sweep.sum()  # clean lines in the cache
@@ -142,7 +155,7 @@ def main():
                 for k in range(K):
                     sts[k].fill_(-1)
                     enc.encode_batch(sid, None, flags, in_off, lens, pays[k], out_off, wires[k], stream, max_len=P,
-                                     nonce_auto=True)
+                                     nonce_auto=True, stream_out=a.enc_stream_out)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
                     dec.decode_batch(sid, out_off, wlen, wires[k], in_off, backs[k], fls[k], sts[k], stream,
