@@ -63,6 +63,9 @@ __device__ __forceinline__ void seq_store4(uint64_t a, uint32_t x, uint32_t y, u
 #ifndef ZMQG_SEQ_COOPST
 #define ZMQG_SEQ_COOPST 2 // k_frames_seq decode under ZMQG_OPT_STREAM_OUT, 64-byte-aligned payloads: each step's chunks stored by the wave cooperatively (16 frames x 64 B per instruction) through LDS, a step later (2; 3: at the next step's top) or at once (1); 0: each lane its own always
 #endif
+#ifndef ZMQG_SEQ_SKIP5
+#define ZMQG_SEQ_SKIP5 1 // LDS-DMA input: no fifth granule for 16-byte-aligned frames (k_frames_seq, k_frames_lds)
+#endif
 #ifndef ZMQG_SEQ_PF
 #define ZMQG_SEQ_PF 1 // k_frames_seq: windows requested ahead of the one computed (1; 2 measured slower)
 #endif
@@ -1405,6 +1408,12 @@ __device__ __forceinline__ void frames_seq_impl(ZMQG_FRAMES_PARAMS)
             sq_rel[j] = 16u * k;
             sq_la[j] = shfl_u64(Ab, f) + sq_rel[j];
             sq_lim[j] = (uint32_t) __shfl((int) lm, (int) f);
+            // (a 16-byte-aligned frame's windows are granules 0..3: its fifth
+            // would be the next window's first, moved twice)
+            // (the shuffle outside the condition: from an inactive lane it reads 0)
+            const int fva = __shfl((int) sq_va, (int) f);
+            if (ZMQG_SEQ_SKIP5 && k == 4u && fva == 0)
+                sq_lim[j] = 0;
         }
     }
     auto sq_dma = [&](uint32_t t) { // window t's covers -> buffer t & 1 (granules holding a stream byte)

@@ -288,6 +288,9 @@ __global__ __launch_bounds__(kFramesBS) void k_frames_lds(
             lrel[j] = 16u * k;
             la[j] = shfl_u64(Ab, f) + lrel[j];
             llim[j] = (uint32_t) __shfl((int) lim, (int) f);
+            const int fva = __shfl((int) va, (int) f); // (k_frames_seq's notes)
+            if (ZMQG_SEQ_SKIP5 && k == 4u && fva == 0)
+                llim[j] = 0;
         }
     }
     // Encode into back-to-back frames (every lane's frame processed, at least
